@@ -1,0 +1,192 @@
+/*
+ * shd_pathengine.h -- C-ABI of the MI355X-native Shadow path engine.
+ *
+ * Drop-in boundary for Shadow v1.14.0 src/main/routing/topology.c.  The
+ * engine replaces the region topology.c:1681-1866 inside
+ * _topology_computeSourcePaths (target collection, the igraph Dijkstra call at
+ * :1765 and the per-target _topology_computePathProperties fold at :1805-1864):
+ * one call returns the dense row for a source, and host C keeps calling
+ * _topology_storePathInCache (:1855) per target, so the cache rules, the
+ * min-latency/lookahead update (:1375-1385) and logging are unchanged.
+ *
+ * Plain C types only (no HIP/torch types).  All functions return 0 on success
+ * or a negative SHD_PE_E* code; shd_pe_strerror() names it.  Caller-owned
+ * input arrays are only borrowed for the duration of the call.  The engine
+ * owns its device memory and stream; nothing it returns outlives
+ * shd_pe_destroy().  The engine never calls back into topology.c.
+ *
+ * Threading: shd_pe_create/compute_* must be serialised by the caller (the
+ * reference holds graphLock around the igraph call, topology.c:1747-1781);
+ * after a row is computed, shd_pe_get_row on it is read-only and may be called
+ * concurrently.
+ */
+#ifndef SHD_PATHENGINE_H
+#define SHD_PATHENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHD_PE_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------ */
+#define SHD_PE_OK            0
+#define SHD_PE_EINVAL       -1   /* bad argument / graph fails topology.c checks  */
+#define SHD_PE_ENOMEM       -2   /* host or device allocation failed              */
+#define SHD_PE_ENODEV       -3   /* no usable gfx950 device / HIP init failed     */
+#define SHD_PE_EUNREACHABLE -4   /* (per entry, see flags) target not reachable    */
+#define SHD_PE_ENOSELFLOOP  -5   /* (per entry, see flags) (s,s) self-loop missing */
+#define SHD_PE_EMULTI       -6   /* parallel edges: multigraphs are rejected       */
+#define SHD_PE_EHIP         -7   /* HIP runtime error during compute               */
+#define SHD_PE_ENOTATTACHED -8   /* vertex is not in the attached set              */
+#define SHD_PE_ENOEDGE      -9   /* direct path requested but (s,t) has no edge    */
+
+/* ---- per-entry flags (uint8) ------------------------------------------ */
+#define SHD_PE_F_UNREACHABLE 0x01u /* igraph could not reach t: not stored         */
+#define SHD_PE_F_NOEDGE      0x02u /* a hop (t==s: the self-loop) has no edge,
+                                      topology.c:1490-1495: not stored            */
+#define SHD_PE_F_ZEROLAT     0x04u /* latency 0 replaced by 1 (topology.c:1848)    */
+#define SHD_PE_F_DIRECT      0x08u /* entry is a direct edge (isDirect=TRUE)       */
+#define SHD_PE_F_EXACT       0x10u /* row had equal-distance predecessor ties and
+                                      was resolved by the on-GPU igraph-heap kernel */
+#define SHD_PE_F_FAILED (SHD_PE_F_UNREACHABLE | SHD_PE_F_NOEDGE)
+
+/* ---- graph description (built once by host C from igraph) ------------- */
+/* Edges in igraph edge-id order (GraphML document order), endpoints as
+ * returned by igraph_edge(); latency/packetLoss are the 'latency' and
+ * 'packetloss' edge attributes (EANV).  vertexPacketLoss is the optional
+ * vertex 'packetloss' attribute (VANV) or NULL when the attribute is absent;
+ * NaN entries mean "value absent" (topology.c:330-349). */
+typedef struct ShdPeGraphDesc {
+    int32_t nVertices;
+    int64_t nEdges;
+    int32_t directed;
+    const int32_t* edgeFrom;
+    const int32_t* edgeTo;
+    const double* edgeLatency;
+    const double* edgePacketLoss;
+    const double* vertexPacketLoss;
+} ShdPeGraphDesc;
+
+/* ---- engine options ---------------------------------------------------- */
+typedef struct ShdPeOptions {
+    int32_t device;          /* HIP device ordinal (one engine per device)        */
+    int32_t batchRows;       /* source rows per launch; 0 = auto                  */
+    double delta;            /* delta-stepping bucket width (ms); 0 = auto        */
+    int32_t storePred;       /* keep a predecessor-vertex column in the table      */
+    int32_t forceMode;       /* 0 auto, 1 sparse delta-stepping, 2 direct gather,
+                                3 exact igraph-heap kernel for every row (tests)  */
+} ShdPeOptions;
+
+typedef struct ShdPe ShdPe;
+
+/* Engine statistics (cumulative since create / reset). */
+typedef struct ShdPeStats {
+    int64_t rowsComputed;
+    int64_t rowsExact;         /* rows resolved by the exact igraph-heap kernel   */
+    int64_t arcsRelaxed;       /* sum over rows of m_arcs (frozen metric formula) */
+    double msSparseKernel;     /* device time of the delta-stepping kernel        */
+    double msExactKernel;      /* device time of the exact (tie) kernel           */
+    double msDirectKernel;     /* device time of the direct-gather kernel         */
+    double msTotal;            /* device time of whole compute calls              */
+    int64_t launchesSparse, launchesExact, launchesDirect;
+    int32_t mode;              /* 1 sparse, 2 direct (complete graph)              */
+    int32_t isComplete;        /* _topology_isComplete() of the graph              */
+    int32_t nVertices;
+    int64_t nArcs;             /* non-loop arcs (undirected edge = 2 arcs)         */
+    int32_t nAttached;
+    double deltaUsed;
+} ShdPeStats;
+
+/* Defaults for ShdPeOptions. */
+void shd_pe_default_options(ShdPeOptions* opt);
+
+/* Build the engine: validates the graph like _topology_checkGraphEdges
+ * (latency > 0, packetloss in [0,1]; topology.c:1041-1124), builds the
+ * CSR in igraph incidence order, uploads it, and fixes the target set =
+ * attached[] (verticesWithAttachedHosts, topology.c:1525-1543; duplicates
+ * removed, first occurrence order kept).  Row/column order of the table is
+ * the order of the unique attached vertices. */
+int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attached,
+                  int32_t nAttached, const ShdPeOptions* opt, ShdPe** out);
+
+void shd_pe_destroy(ShdPe* pe);
+
+const char* shd_pe_strerror(int code);
+
+/* _topology_isComplete (topology.c:450-552) on the uploaded graph. */
+int shd_pe_is_complete(const ShdPe* pe);
+
+/* Number of unique attached vertices (T) and their order. */
+int32_t shd_pe_num_attached(const ShdPe* pe);
+int shd_pe_attached(const ShdPe* pe, int32_t* outVertices);
+
+/* Compute all rows (eager batch, e.g. on the first cache miss). */
+int shd_pe_compute_all(ShdPe* pe);
+
+/* Compute rows for the given sources (vertex ids, must be attached). */
+int shd_pe_compute_rows(ShdPe* pe, const int32_t* srcVertices, int32_t count);
+
+/* Compute rows by table position (0..T-1), e.g. a shard [start, start+count). */
+int shd_pe_compute_positions(ShdPe* pe, int32_t start, int32_t count);
+
+/* Copy the row of source srcVertex (computing it if needed) into caller
+ * buffers of T entries in attached order.  Any pointer may be NULL.
+ * lat/rel follow _topology_computePathProperties exactly; hops = edges folded
+ * (1 for t == s: the self-loop); pred = vertex before t (-1 for t == s,
+ * needs storePred); flags = SHD_PE_F_*.  For a complete graph the row holds
+ * the direct-edge values (_topology_lookupDirectPath, topology.c:1877-1927). */
+int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double* rel,
+                   int32_t* hops, int32_t* pred, uint8_t* flags);
+
+/* Copy rows [start, start+count) (table positions) of the device table into
+ * caller DEVICE buffers (e.g. an RCCL all-gather staging area).  Row-major,
+ * T entries per row.  Any pointer may be NULL. */
+int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count,
+                            double* dLat, double* dRel, int32_t* dHops,
+                            uint8_t* dFlags);
+
+/* Wait for outstanding device work of this engine. */
+int shd_pe_synchronize(ShdPe* pe);
+
+int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out);
+int shd_pe_reset_stats(ShdPe* pe);
+
+/* ---- host-side helpers Shadow keeps in C (no GPU work) ----------------- */
+/* _topology_lookupDirectPath (topology.c:1877-1927) for one pair. */
+int shd_pe_direct_path(const ShdPe* pe, int32_t s, int32_t t, double* lat, double* rel);
+/* _topology_computeShortestPathToSelf (topology.c:1545-1653). */
+int shd_pe_self_path(const ShdPe* pe, int32_t v, double* lat, double* rel);
+/* _topology_verticesAreAdjacent (topology.c:1248-1264): 1, 0. */
+int shd_pe_adjacent(const ShdPe* pe, int32_t s, int32_t t);
+
+/* ------------------------------------------------------------------------
+ * Host mirror of the topology.c path API (the drop-in seen by worker.c,
+ * tcp.c, host.c): _topology_getPathEntry + the two-level path cache, with
+ * rows coming from the engine.  Queries are by vertex index; Shadow's
+ * Address -> vertex map (topology.c:1388-1405) stays where it is.
+ * ---------------------------------------------------------------------- */
+typedef struct ShdTopology ShdTopology;
+
+int shd_topology_new(ShdPe* pe, int32_t prefersDirectPaths, ShdTopology** out);
+void shd_topology_free(ShdTopology* top);
+/* topology_getLatency / getReliability (topology.c:2065-2087): -1 on error. */
+double shd_topology_get_latency(ShdTopology* top, int32_t srcV, int32_t dstV);
+double shd_topology_get_reliability(ShdTopology* top, int32_t srcV, int32_t dstV);
+/* topology_isRoutable (topology.c:2089-2092). */
+int shd_topology_is_routable(ShdTopology* top, int32_t srcV, int32_t dstV);
+/* topology_incrementPathPacketCounter (topology.c:2053-2063): 0 / -1. */
+int shd_topology_increment_path_packet_counter(ShdTopology* top, int32_t srcV, int32_t dstV);
+/* Inspect the cache entry stored under (src,dst): 1 present, 0 absent. */
+int shd_topology_cached(const ShdTopology* top, int32_t srcV, int32_t dstV,
+                        double* lat, double* rel, int32_t* isDirect, int64_t* packetCount);
+double shd_topology_min_latency(const ShdTopology* top);
+int64_t shd_topology_cache_size(const ShdTopology* top);
+int64_t shd_topology_rows_computed(const ShdTopology* top);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,89 @@
+// pe_device.hpp -- device-side data layout shared by the engine and kernels.
+//
+// HBM layout (one engine = one device):
+//   graph  : CSR of OUT arcs without self-loops, rows sorted by neighbour id
+//            (= igraph incidence order); SoA arrays
+//            col[i32] lat[f64] rel[f64] (rel = 1.0 - packetloss, topology.c:437).
+//            For directed graphs an IN-arc CSR (inCol/inLat/inRel) is kept for
+//            the predecessor pass; undirected graphs alias it to the OUT CSR.
+//   vertex : vrel[f64] (1 - vertex packetloss, 1.0 when absent/NaN),
+//            self-loop latency/rel + hasSelf (the (s,s) hop, topology.c:1469).
+//   table  : row-major [T rows][T cols] lat f64 | rel f64 | hops i32 |
+//            flags u8 (| pred i32 optional), row/col order = attached[].
+//   scratch: one slot per resident workgroup: dist f64, hops i32, rel f64,
+//            pred i32 (+ heap key/idx, index2 for the exact kernel).
+#pragma once
+#include <stdint.h>
+
+namespace shdpe {
+
+struct DevGraph {
+    int32_t n;
+    int32_t T;                 // unique attached vertices (= targets)
+    const int32_t* rowPtr;     // [n+1]
+    const int32_t* col;        // [nArcs]
+    const double* lat;
+    const double* rel;
+    const int32_t* inPtr;      // [n+1] (aliases rowPtr when undirected)
+    const int32_t* inCol;
+    const double* inLat;
+    const double* inRel;
+    const int32_t* outToIn;    // out arc u->v  ->  index of that edge in v's IN list
+    const double* vrel;        // [n]
+    const double* selfLat;     // [n]
+    const double* selfRel;     // [n]
+    const uint8_t* hasSelf;    // [n]
+    const int32_t* attached;   // [T]
+    const uint8_t* isAttached; // [n]
+};
+
+struct DevTable {
+    double* lat;
+    double* rel;
+    int32_t* hops;
+    int32_t* pred;     // may be null
+    uint8_t* flags;
+    int64_t T;
+};
+
+struct DevScratch {
+    double* dist;      // exact kernel: final distance at pop
+    int32_t* hops;
+    double* rel;
+    int32_t* pred;     // IN-arc index of the chosen predecessor edge, -1 none
+    double* heapKey;   // exact kernel 2-way heap (igraph_2wheap_t data)
+    int32_t* heapIdx;  // exact kernel 2-way heap (index)
+    int32_t* index2;   // exact kernel: 0 never reached, 1 popped, >=2 heap pos+2
+    int64_t stride;    // elements per slot (>= n)
+};
+
+// per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)
+constexpr uint8_t F_UNREACHABLE = 0x01;
+constexpr uint8_t F_NOEDGE = 0x02;
+constexpr uint8_t F_ZEROLAT = 0x04;
+constexpr uint8_t F_DIRECT = 0x08;
+constexpr uint8_t F_EXACT = 0x10;
+
+struct SparseLaunch {
+    int32_t threads;     // workgroup size
+    int32_t grid;        // persistent workgroups (= scratch slots)
+    int32_t ldsBytes;    // dynamic LDS
+    int32_t qcap;        // light frontier queue capacity
+    int32_t hcap;        // heavy (wave-per-vertex) queue capacity
+    int32_t heavyDeg;    // degree threshold for the heavy queue
+    bool ldsDist;        // dist array in LDS (n small enough)
+    double delta;        // bucket width
+};
+
+// kernels (pe_kernels.hip); all launched on `stream`.
+void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                        const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
+                        const SparseLaunch& cfg, void* stream);
+void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                       const int32_t* dRows, int32_t nRows, int32_t grid, bool ldsIndex,
+                       void* stream);
+void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
+                        int32_t nRows, void* stream);
+int sparse_max_threads();
+
+}  // namespace shdpe

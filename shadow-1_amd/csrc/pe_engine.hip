@@ -1,0 +1,468 @@
+// pe_engine.hip -- C-ABI implementation of the MI355X Shadow path engine.
+//
+// Replaces topology.c:1681-1866 (target collection + igraph Dijkstra +
+// per-target fold) with device kernels; see include/shd_pathengine.h.
+// No CPU compute fallback: every row comes from a gfx950 kernel, and create
+// fails with SHD_PE_ENODEV when no device is usable.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "pe_device.hpp"
+#include "pe_graph.hpp"
+#include "shd_pathengine.h"
+
+using namespace shdpe;
+
+struct ShdPe {
+    HostGraph hg;
+    std::vector<int32_t> attached;   // unique, first-occurrence order
+    std::vector<int32_t> posOf;      // vertex -> table position or -1
+    ShdPeOptions opt{};
+    int device = 0;
+    int numCUs = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evA = nullptr, evB = nullptr;
+    std::vector<void*> allocs;
+    DevGraph dg{};
+    DevTable tab{};
+    DevScratch sc{};
+    bool tableReady = false;
+    int32_t* dRows = nullptr;
+    uint8_t* dRowAmbig = nullptr;
+    int32_t rowsCap = 0;
+    SparseLaunch cfg{};
+    int exactGrid = 0;
+    bool exactLdsIdx = false;
+    int mode = 1;
+    std::vector<uint8_t> rowDone;
+    ShdPeStats stats{};
+    std::mutex mu;
+};
+
+#define HIPCHK(x)                                   \
+    do {                                            \
+        if ((x) != hipSuccess) return SHD_PE_EHIP;  \
+    } while (0)
+
+static int dev_alloc(ShdPe* pe, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc(p, bytes) != hipSuccess) { *p = nullptr; return SHD_PE_ENOMEM; }
+    pe->allocs.push_back(*p);
+    return SHD_PE_OK;
+}
+
+template <class T>
+static int dev_upload(ShdPe* pe, T** dst, const std::vector<T>& src) {
+    int rc = dev_alloc(pe, reinterpret_cast<void**>(dst), src.size() * sizeof(T));
+    if (rc) return rc;
+    if (!src.empty())
+        HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SHD_PE_OK;
+}
+
+static double env_double(const char* name, double dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atof(v) : dflt;
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+extern "C" void shd_pe_default_options(ShdPeOptions* opt) {
+    if (!opt) return;
+    std::memset(opt, 0, sizeof(*opt));
+    opt->device = 0;
+    opt->batchRows = 0;
+    opt->delta = 0.0;
+    opt->storePred = 1;
+    opt->forceMode = 0;
+}
+
+extern "C" const char* shd_pe_strerror(int code) {
+    switch (code) {
+        case SHD_PE_OK: return "ok";
+        case SHD_PE_EINVAL: return "invalid argument or graph fails topology checks";
+        case SHD_PE_ENOMEM: return "out of memory";
+        case SHD_PE_ENODEV: return "no usable gfx950 device";
+        case SHD_PE_EUNREACHABLE: return "target unreachable";
+        case SHD_PE_ENOSELFLOOP: return "self-loop (s,s) missing";
+        case SHD_PE_EMULTI: return "parallel edges (multigraph) are not supported";
+        case SHD_PE_EHIP: return "HIP runtime error";
+        case SHD_PE_ENOTATTACHED: return "vertex is not attached";
+        case SHD_PE_ENOEDGE: return "no edge between the vertices";
+        default: return "unknown error";
+    }
+}
+
+static void configure(ShdPe* pe) {
+    const HostGraph& g = pe->hg;
+    const int n = g.n;
+    const int nw = (n + 31) / 32;
+    const int LDS = 160 * 1024;
+    SparseLaunch c{};
+    c.threads = env_int("SHDPE_THREADS", 512);
+    if (c.threads > sparse_max_threads()) c.threads = sparse_max_threads();
+    c.hcap = 256;
+    c.heavyDeg = env_int("SHDPE_HEAVY_DEG", 64);
+    const int fixedPend = 64 + ((4 * nw + 15) & ~15) + 4 * c.hcap;
+    const int qmin = 4096;
+    c.ldsDist = (fixedPend + 8 * n + 4 * qmin) <= LDS && env_int("SHDPE_NO_LDS_DIST", 0) == 0;
+    int room = LDS - fixedPend - (c.ldsDist ? 8 * n : 0);
+    c.qcap = std::min(room / 4, std::max(n, 1024));
+    if (c.qcap < 256) c.qcap = 256;
+    c.ldsBytes = fixedPend + (c.ldsDist ? 8 * n : 0) + 4 * c.qcap;
+    int wgPerCU = std::max(1, std::min(4, LDS / std::max(c.ldsBytes, 1)));
+    c.grid = pe->numCUs * wgPerCU;
+    double factor = env_double("SHDPE_DELTA_FACTOR", 4.0);
+    c.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * factor;
+    if (!(c.delta > 0)) c.delta = 1.0;
+    pe->cfg = c;
+    pe->exactLdsIdx = (size_t)4 * n <= 64 * 1024;
+    int exPerCU = pe->exactLdsIdx ? std::max(1, std::min(8, LDS / std::max(4 * n, 1))) : 8;
+    pe->exactGrid = pe->numCUs * exPerCU;
+    pe->stats.deltaUsed = c.delta;
+}
+
+extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attached,
+                             int32_t nAttached, const ShdPeOptions* opt, ShdPe** out) {
+    if (!out || !graph || nAttached <= 0 || !attached) return SHD_PE_EINVAL;
+    *out = nullptr;
+    ShdPe* pe = new (std::nothrow) ShdPe();
+    if (!pe) return SHD_PE_ENOMEM;
+    if (opt) pe->opt = *opt; else shd_pe_default_options(&pe->opt);
+    int rc = build_host_graph(graph, &pe->hg);
+    if (rc) { delete pe; return rc; }
+    const HostGraph& g = pe->hg;
+    pe->posOf.assign(g.n, -1);
+    for (int32_t i = 0; i < nAttached; ++i) {
+        const int32_t v = attached[i];
+        if (v < 0 || v >= g.n) { delete pe; return SHD_PE_EINVAL; }
+        if (pe->posOf[v] < 0) {
+            pe->posOf[v] = (int32_t)pe->attached.size();
+            pe->attached.push_back(v);
+        }
+    }
+    // ---- device ----
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || pe->opt.device < 0 ||
+        pe->opt.device >= ndev) {
+        delete pe;
+        return SHD_PE_ENODEV;
+    }
+    pe->device = pe->opt.device;
+    if (hipSetDevice(pe->device) != hipSuccess) { delete pe; return SHD_PE_ENODEV; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, pe->device) != hipSuccess) { delete pe; return SHD_PE_ENODEV; }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) { delete pe; return SHD_PE_ENODEV; }
+    pe->numCUs = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&pe->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&pe->ev0) != hipSuccess || hipEventCreate(&pe->ev1) != hipSuccess ||
+        hipEventCreate(&pe->evA) != hipSuccess || hipEventCreate(&pe->evB) != hipSuccess) {
+        shd_pe_destroy(pe);
+        return SHD_PE_ENODEV;
+    }
+    configure(pe);
+    const int32_t T = (int32_t)pe->attached.size();
+    DevGraph& d = pe->dg;
+    d.n = g.n;
+    d.T = T;
+    std::vector<uint8_t> isAtt(g.n, 0);
+    for (int32_t v : pe->attached) isAtt[v] = 1;
+    int32_t *rowPtr, *col, *outToIn, *att;
+    double *lat, *rel, *vrel, *sl, *sr;
+    uint8_t *hs, *ia;
+    if ((rc = dev_upload(pe, &rowPtr, g.rowPtr)) || (rc = dev_upload(pe, &col, g.col)) ||
+        (rc = dev_upload(pe, &lat, g.lat)) || (rc = dev_upload(pe, &rel, g.rel)) ||
+        (rc = dev_upload(pe, &outToIn, g.outToIn)) || (rc = dev_upload(pe, &vrel, g.vrel)) ||
+        (rc = dev_upload(pe, &sl, g.selfLat)) || (rc = dev_upload(pe, &sr, g.selfRel)) ||
+        (rc = dev_upload(pe, &hs, g.hasSelf)) || (rc = dev_upload(pe, &att, pe->attached)) ||
+        (rc = dev_upload(pe, &ia, isAtt))) {
+        shd_pe_destroy(pe);
+        return rc;
+    }
+    d.rowPtr = rowPtr; d.col = col; d.lat = lat; d.rel = rel; d.outToIn = outToIn;
+    d.vrel = vrel; d.selfLat = sl; d.selfRel = sr; d.hasSelf = hs; d.attached = att;
+    d.isAttached = ia;
+    if (g.directed) {
+        int32_t *ip, *ic;
+        double *il, *ir;
+        if ((rc = dev_upload(pe, &ip, g.inPtr)) || (rc = dev_upload(pe, &ic, g.inCol)) ||
+            (rc = dev_upload(pe, &il, g.inLat)) || (rc = dev_upload(pe, &ir, g.inRel))) {
+            shd_pe_destroy(pe);
+            return rc;
+        }
+        d.inPtr = ip; d.inCol = ic; d.inLat = il; d.inRel = ir;
+    } else {
+        d.inPtr = rowPtr; d.inCol = col; d.inLat = lat; d.inRel = rel;
+    }
+    pe->mode = (g.isComplete && pe->opt.forceMode != 1 && pe->opt.forceMode != 3) ? 2 : 1;
+    if (pe->opt.forceMode == 2) pe->mode = 2;
+    pe->rowDone.assign(T, 0);
+    pe->stats.mode = pe->mode;
+    pe->stats.isComplete = g.isComplete ? 1 : 0;
+    pe->stats.nVertices = g.n;
+    pe->stats.nArcs = g.nArcs();
+    pe->stats.nAttached = T;
+    *out = pe;
+    return SHD_PE_OK;
+}
+
+static int ensure_table(ShdPe* pe) {
+    if (pe->tableReady) return SHD_PE_OK;
+    const size_t T = pe->attached.size();
+    const size_t cells = T * T;
+    int rc;
+    void *lat, *rel, *hops, *flags, *pred = nullptr;
+    if ((rc = dev_alloc(pe, &lat, cells * 8)) || (rc = dev_alloc(pe, &rel, cells * 8)) ||
+        (rc = dev_alloc(pe, &hops, cells * 4)) || (rc = dev_alloc(pe, &flags, cells)))
+        return rc;
+    if (pe->opt.storePred && (rc = dev_alloc(pe, &pred, cells * 4))) return rc;
+    pe->tab.lat = (double*)lat;
+    pe->tab.rel = (double*)rel;
+    pe->tab.hops = (int32_t*)hops;
+    pe->tab.flags = (uint8_t*)flags;
+    pe->tab.pred = (int32_t*)pred;
+    pe->tab.T = (int64_t)T;
+    // scratch slots
+    const int slots = std::max(pe->cfg.grid, pe->exactGrid);
+    const size_t stride = ((size_t)pe->hg.n + 63) & ~(size_t)63;
+    void *dist, *sh, *sr, *sp, *hk, *hi, *i2;
+    if ((rc = dev_alloc(pe, &dist, slots * stride * 8)) ||
+        (rc = dev_alloc(pe, &sh, slots * stride * 4)) ||
+        (rc = dev_alloc(pe, &sr, slots * stride * 8)) ||
+        (rc = dev_alloc(pe, &sp, slots * stride * 4)) ||
+        (rc = dev_alloc(pe, &hk, (size_t)pe->exactGrid * stride * 8)) ||
+        (rc = dev_alloc(pe, &hi, (size_t)pe->exactGrid * stride * 4)) ||
+        (rc = dev_alloc(pe, &i2, pe->exactLdsIdx ? 16 : (size_t)pe->exactGrid * stride * 4)))
+        return rc;
+    pe->sc.dist = (double*)dist;
+    pe->sc.hops = (int32_t*)sh;
+    pe->sc.rel = (double*)sr;
+    pe->sc.pred = (int32_t*)sp;
+    pe->sc.heapKey = (double*)hk;
+    pe->sc.heapIdx = (int32_t*)hi;
+    pe->sc.index2 = (int32_t*)i2;
+    pe->sc.stride = (int64_t)stride;
+    pe->rowsCap = (int32_t)std::min<size_t>(T, 1 << 20);
+    void *rows, *amb;
+    if ((rc = dev_alloc(pe, &rows, (size_t)pe->rowsCap * 4)) ||
+        (rc = dev_alloc(pe, &amb, (size_t)pe->rowsCap)))
+        return rc;
+    pe->dRows = (int32_t*)rows;
+    pe->dRowAmbig = (uint8_t*)amb;
+    pe->tableReady = true;
+    return SHD_PE_OK;
+}
+
+static float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
+
+// Compute the given table positions (chunked); caller holds pe->mu.
+static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count) {
+    if (count <= 0) return SHD_PE_OK;
+    if (hipSetDevice(pe->device) != hipSuccess) return SHD_PE_EHIP;
+    int rc = ensure_table(pe);
+    if (rc) return rc;
+    std::vector<uint8_t> amb;
+    std::vector<int32_t> exactRows;
+    HIPCHK(hipEventRecord(pe->ev0, pe->stream));
+    for (int32_t c0 = 0; c0 < count; c0 += pe->rowsCap) {
+        const int32_t cnt = std::min(pe->rowsCap, count - c0);
+        HIPCHK(hipMemcpyAsync(pe->dRows, pos + c0, (size_t)cnt * 4, hipMemcpyHostToDevice,
+                              pe->stream));
+        exactRows.clear();
+        if (pe->mode == 2) {
+            HIPCHK(hipEventRecord(pe->evA, pe->stream));
+            launch_direct_rows(pe->dg, pe->tab, pe->dRows, cnt, pe->stream);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(pe->evB, pe->stream));
+            HIPCHK(hipEventSynchronize(pe->evB));
+            pe->stats.msDirectKernel += elapsed(pe->evA, pe->evB);
+            pe->stats.launchesDirect++;
+        } else if (pe->opt.forceMode == 3) {
+            exactRows.assign(pos + c0, pos + c0 + cnt);
+        } else {
+            HIPCHK(hipEventRecord(pe->evA, pe->stream));
+            launch_sparse_rows(pe->dg, pe->tab, pe->sc, pe->dRows, cnt, pe->dRowAmbig, pe->cfg,
+                               pe->stream);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(pe->evB, pe->stream));
+            amb.resize(cnt);
+            HIPCHK(hipMemcpyAsync(amb.data(), pe->dRowAmbig, cnt, hipMemcpyDeviceToHost,
+                                  pe->stream));
+            HIPCHK(hipStreamSynchronize(pe->stream));
+            pe->stats.msSparseKernel += elapsed(pe->evA, pe->evB);
+            pe->stats.launchesSparse++;
+            for (int32_t i = 0; i < cnt; ++i)
+                if (amb[i]) exactRows.push_back(pos[c0 + i]);
+        }
+        if (!exactRows.empty()) {
+            HIPCHK(hipMemcpyAsync(pe->dRows, exactRows.data(), exactRows.size() * 4,
+                                  hipMemcpyHostToDevice, pe->stream));
+            HIPCHK(hipEventRecord(pe->evA, pe->stream));
+            launch_exact_rows(pe->dg, pe->tab, pe->sc, pe->dRows, (int32_t)exactRows.size(),
+                              pe->exactGrid, pe->exactLdsIdx, pe->stream);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(pe->evB, pe->stream));
+            HIPCHK(hipEventSynchronize(pe->evB));
+            pe->stats.msExactKernel += elapsed(pe->evA, pe->evB);
+            pe->stats.launchesExact++;
+            pe->stats.rowsExact += (int64_t)exactRows.size();
+        }
+    }
+    HIPCHK(hipEventRecord(pe->ev1, pe->stream));
+    HIPCHK(hipEventSynchronize(pe->ev1));
+    pe->stats.msTotal += elapsed(pe->ev0, pe->ev1);
+    pe->stats.rowsComputed += count;
+    pe->stats.arcsRelaxed += (int64_t)count * pe->hg.nArcs();
+    for (int32_t i = 0; i < count; ++i) pe->rowDone[pos[i]] = 1;
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_compute_positions(ShdPe* pe, int32_t start, int32_t count) {
+    if (!pe || start < 0 || count < 0 || (int64_t)start + count > (int64_t)pe->attached.size())
+        return SHD_PE_EINVAL;
+    std::vector<int32_t> pos(count);
+    for (int32_t i = 0; i < count; ++i) pos[i] = start + i;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    return compute_positions_locked(pe, pos.data(), count);
+}
+
+extern "C" int shd_pe_compute_all(ShdPe* pe) {
+    if (!pe) return SHD_PE_EINVAL;
+    return shd_pe_compute_positions(pe, 0, (int32_t)pe->attached.size());
+}
+
+extern "C" int shd_pe_compute_rows(ShdPe* pe, const int32_t* src, int32_t count) {
+    if (!pe || count < 0 || (count > 0 && !src)) return SHD_PE_EINVAL;
+    std::vector<int32_t> pos(count);
+    for (int32_t i = 0; i < count; ++i) {
+        if (src[i] < 0 || src[i] >= pe->hg.n || pe->posOf[src[i]] < 0) return SHD_PE_ENOTATTACHED;
+        pos[i] = pe->posOf[src[i]];
+    }
+    std::lock_guard<std::mutex> lk(pe->mu);
+    return compute_positions_locked(pe, pos.data(), count);
+}
+
+extern "C" int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double* rel,
+                              int32_t* hops, int32_t* pred, uint8_t* flags) {
+    if (!pe || srcVertex < 0 || srcVertex >= pe->hg.n) return SHD_PE_EINVAL;
+    const int32_t p = pe->posOf[srcVertex];
+    if (p < 0) return SHD_PE_ENOTATTACHED;
+    if (pred && !pe->opt.storePred) return SHD_PE_EINVAL;
+    if (!pe->rowDone[p]) {
+        std::lock_guard<std::mutex> lk(pe->mu);
+        if (!pe->rowDone[p]) {
+            int rc = compute_positions_locked(pe, &p, 1);
+            if (rc) return rc;
+        }
+    }
+    if (hipSetDevice(pe->device) != hipSuccess) return SHD_PE_EHIP;
+    const size_t T = pe->attached.size(), off = (size_t)p * T;
+    if (lat) HIPCHK(hipMemcpy(lat, pe->tab.lat + off, T * 8, hipMemcpyDeviceToHost));
+    if (rel) HIPCHK(hipMemcpy(rel, pe->tab.rel + off, T * 8, hipMemcpyDeviceToHost));
+    if (hops) HIPCHK(hipMemcpy(hops, pe->tab.hops + off, T * 4, hipMemcpyDeviceToHost));
+    if (pred) HIPCHK(hipMemcpy(pred, pe->tab.pred + off, T * 4, hipMemcpyDeviceToHost));
+    if (flags) HIPCHK(hipMemcpy(flags, pe->tab.flags + off, T, hipMemcpyDeviceToHost));
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, double* dLat,
+                                       double* dRel, int32_t* dHops, uint8_t* dFlags) {
+    if (!pe || start < 0 || count < 0 || (int64_t)start + count > (int64_t)pe->attached.size())
+        return SHD_PE_EINVAL;
+    if (!pe->tableReady) return SHD_PE_EINVAL;
+    const size_t T = pe->attached.size(), off = (size_t)start * T, cells = (size_t)count * T;
+    HIPCHK(hipSetDevice(pe->device));
+    if (dLat) HIPCHK(hipMemcpyAsync(dLat, pe->tab.lat + off, cells * 8, hipMemcpyDeviceToDevice, pe->stream));
+    if (dRel) HIPCHK(hipMemcpyAsync(dRel, pe->tab.rel + off, cells * 8, hipMemcpyDeviceToDevice, pe->stream));
+    if (dHops) HIPCHK(hipMemcpyAsync(dHops, pe->tab.hops + off, cells * 4, hipMemcpyDeviceToDevice, pe->stream));
+    if (dFlags) HIPCHK(hipMemcpyAsync(dFlags, pe->tab.flags + off, cells, hipMemcpyDeviceToDevice, pe->stream));
+    HIPCHK(hipStreamSynchronize(pe->stream));
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_synchronize(ShdPe* pe) {
+    if (!pe) return SHD_PE_EINVAL;
+    HIPCHK(hipSetDevice(pe->device));
+    HIPCHK(hipStreamSynchronize(pe->stream));
+    return SHD_PE_OK;
+}
+
+extern "C" void shd_pe_destroy(ShdPe* pe) {
+    if (!pe) return;
+    if (!pe->allocs.empty() || pe->stream) (void)hipSetDevice(pe->device);
+    if (pe->stream) (void)hipStreamSynchronize(pe->stream);
+    for (void* p : pe->allocs) (void)hipFree(p);
+    if (pe->ev0) (void)hipEventDestroy(pe->ev0);
+    if (pe->ev1) (void)hipEventDestroy(pe->ev1);
+    if (pe->evA) (void)hipEventDestroy(pe->evA);
+    if (pe->evB) (void)hipEventDestroy(pe->evB);
+    if (pe->stream) (void)hipStreamDestroy(pe->stream);
+    delete pe;
+}
+
+extern "C" int shd_pe_is_complete(const ShdPe* pe) { return pe && pe->hg.isComplete ? 1 : 0; }
+
+extern "C" int32_t shd_pe_num_attached(const ShdPe* pe) {
+    return pe ? (int32_t)pe->attached.size() : 0;
+}
+
+extern "C" int shd_pe_attached(const ShdPe* pe, int32_t* out) {
+    if (!pe || !out) return SHD_PE_EINVAL;
+    std::memcpy(out, pe->attached.data(), pe->attached.size() * sizeof(int32_t));
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
+    if (!pe || !out) return SHD_PE_EINVAL;
+    *out = pe->stats;
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_reset_stats(ShdPe* pe) {
+    if (!pe) return SHD_PE_EINVAL;
+    ShdPeStats keep = pe->stats;
+    std::memset(&pe->stats, 0, sizeof(pe->stats));
+    pe->stats.mode = keep.mode;
+    pe->stats.isComplete = keep.isComplete;
+    pe->stats.nVertices = keep.nVertices;
+    pe->stats.nArcs = keep.nArcs;
+    pe->stats.nAttached = keep.nAttached;
+    pe->stats.deltaUsed = keep.deltaUsed;
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_direct_path(const ShdPe* pe, int32_t s, int32_t t, double* lat,
+                                  double* rel) {
+    if (!pe) return SHD_PE_EINVAL;
+    return host_direct_path(pe->hg, s, t, lat, rel);
+}
+
+extern "C" int shd_pe_self_path(const ShdPe* pe, int32_t v, double* lat, double* rel) {
+    if (!pe) return SHD_PE_EINVAL;
+    return host_self_path(pe->hg, v, lat, rel);
+}
+
+extern "C" int shd_pe_adjacent(const ShdPe* pe, int32_t s, int32_t t) {
+    if (!pe) return 0;
+    return pe->hg.findArc(s, t) != -1 ? 1 : 0;
+}
+
+// exported for the host topology mirror (pe_topology.cpp)
+const shdpe::HostGraph* shd_pe_host_graph(const ShdPe* pe) { return pe ? &pe->hg : nullptr; }
+int32_t shd_pe_position(const ShdPe* pe, int32_t v) {
+    return (pe && v >= 0 && v < pe->hg.n) ? pe->posOf[v] : -1;
+}

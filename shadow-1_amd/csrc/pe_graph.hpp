@@ -1,0 +1,45 @@
+// pe_graph.hpp -- host-side graph model of the engine (no GPU types).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "shd_pathengine.h"
+
+namespace shdpe {
+
+// CSR in igraph incidence order (ascending neighbour id) with self-loops
+// split out.  Built from the igraph edge list handed over the C-ABI.
+struct HostGraph {
+    int32_t n = 0;
+    int32_t directed = 0;
+    int64_t nEdges = 0;
+    // OUT arcs without self-loops
+    std::vector<int32_t> rowPtr, col;
+    std::vector<double> lat, rel;
+    // IN arcs (directed only; undirected uses the OUT arrays)
+    std::vector<int32_t> inPtr, inCol;
+    std::vector<double> inLat, inRel;
+    std::vector<int32_t> outToIn;
+    // vertex data
+    std::vector<double> vrel;       // 1 - packetloss, 1.0 when absent/NaN
+    std::vector<double> selfLat, selfRel;
+    std::vector<uint8_t> hasSelf;
+    bool isComplete = false;
+    double meanArcLatency = 0.0;
+
+    int64_t nArcs() const { return (int64_t)col.size(); }
+    // igraph_get_eid(from,to) restricted to simple graphs: arc index into the
+    // OUT arrays, -2 for the self-loop, -1 for none.
+    int64_t findArc(int32_t from, int32_t to) const;
+};
+
+// Validate + build (topology.c:1041-1124 checks, igraph_add_edges order).
+int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g);
+
+// _topology_lookupDirectPath (topology.c:1877-1927)
+int host_direct_path(const HostGraph& g, int32_t s, int32_t t, double* lat, double* rel);
+// _topology_computeShortestPathToSelf (topology.c:1545-1653)
+int host_self_path(const HostGraph& g, int32_t v, double* lat, double* rel);
+
+}  // namespace shdpe

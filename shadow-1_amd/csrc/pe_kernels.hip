@@ -1,0 +1,593 @@
+// pe_kernels.hip -- gfx950 kernels of the Shadow path engine.
+//
+// Reference semantics (Shadow v1.14.0, src/main/routing/topology.c):
+//   row      = _topology_computeSourcePaths            :1655-1875
+//   SSSP     = igraph_get_shortest_paths_dijkstra      :1765 (igraph 0.7.1)
+//   fold     = _topology_computePathProperties         :1407-1523
+//   direct   = _topology_lookupDirectPath              :1877-1927
+//
+// Three kernels:
+//   k_sparse_rows  one workgroup per source row: delta-stepping label-
+//                  correcting SSSP with dist in LDS (u64 bit patterns of the
+//                  positive doubles -> ds_min_rtn_u64), pending bitmask + LDS
+//                  frontier queues (thread-per-vertex, wave-per-vertex for
+//                  hubs), then a predecessor pass (tight in-arc with minimum
+//                  dist[u] = igraph's first-popped tight predecessor), an
+//                  equal-distance tie detector, label verification/fix-up and
+//                  the row writer.  Relaxations are dist[u] + w (left fold) so
+//                  the fixpoint is bit-identical to igraph's distances
+//                  (SURVEY.md Appendix B).
+//   k_exact_rows   one wavefront per tie-ambiguous row: igraph 0.7.1 2-way
+//                  heap Dijkstra emulated exactly (lane 0 owns the heap, the
+//                  wave stages the popped vertex's arcs in registers and
+//                  broadcasts them with ds_bpermute).
+//   k_direct_rows  complete graphs: direct-edge gather (HBM-bound).
+#include <hip/hip_runtime.h>
+
+#include "pe_device.hpp"
+
+namespace shdpe {
+
+constexpr unsigned long long INF_BITS = 0x7FF0000000000000ull;
+constexpr int SP_THREADS = 512;
+constexpr int EX_THREADS = 64;
+
+__device__ __forceinline__ double b2d(unsigned long long b) {
+    return __longlong_as_double((long long)b);
+}
+__device__ __forceinline__ unsigned long long d2b(double d) {
+    return (unsigned long long)__double_as_longlong(d);
+}
+
+__device__ __forceinline__ unsigned long long ld_relaxed(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
+struct alignas(16) Ctrl {
+    int qtail[2];
+    int htail[2];
+    unsigned long long minNext[2];
+    int ambig;
+    int mismatch;
+    int changed;
+    int pad;
+    double pad2;
+};
+static_assert(sizeof(Ctrl) <= 64, "ctrl block");
+
+// Forward fold of reliability with vertex factors (topology.c:1430-1462,
+// :1499) for entries where a_s * a_t != 1: walk the chosen predecessor chain
+// back to s, then multiply in source->target order.
+__device__ __noinline__ double fold_rel_general(const DevGraph& g, const int32_t* P, int s, int t,
+                                                int h) {
+    double acc = 1.0 * g.vrel[s];
+    acc = acc * g.vrel[t];
+    if (h <= 64) {
+        double fac[64];
+        int k = 0, x = t;
+        while (x != s && k < 64) {
+            int a = P[x];
+            fac[k++] = g.inRel[a];
+            x = g.inCol[a];
+        }
+        for (int i = k - 1; i >= 0; --i) acc = acc * fac[i];
+        return acc;
+    }
+    // long chains: O(h^2) re-walk, exact order, no scratch
+    for (int d = 1; d <= h; ++d) {
+        int x = t;
+        for (int up = 0; up < h - d; ++up) x = g.inCol[P[x]];
+        acc = acc * g.inRel[P[x]];
+    }
+    return acc;
+}
+
+// Row writer shared by the sparse and exact kernels (topology.c:1805-1864).
+template <class DistOf>
+__device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab, int r, int s,
+                                         DistOf distOf, const int32_t* H, const double* R,
+                                         const int32_t* P, uint8_t extra, int tid, int NT) {
+    const int64_t T = tab.T;
+    const size_t base = (size_t)r * (size_t)T;
+    for (int j = tid; j < T; j += NT) {
+        const int t = g.attached[j];
+        double L = 0.0, Rl = 0.0;
+        int h = -1, pv = -1;
+        uint8_t f = extra;
+        if (t == s) {
+            // 1-vertex igraph path [s]: the fold uses edge (s,s) (:1469-1488),
+            // the destination factor is skipped (:1457).
+            if (g.hasSelf[s]) {
+                L = 0.0 + g.selfLat[s];
+                Rl = (1.0 * g.vrel[s]) * g.selfRel[s];
+                h = 1;
+            } else {
+                f |= F_NOEDGE;
+            }
+        } else {
+            const unsigned long long db = distOf(t);
+            if (db == INF_BITS) {
+                f |= F_UNREACHABLE;
+            } else {
+                L = b2d(db);
+                h = H[t];
+                const int pa = P[t];
+                pv = g.inCol[pa];
+                if (g.vrel[s] == 1.0 && g.vrel[t] == 1.0) Rl = R[t];
+                else Rl = fold_rel_general(g, P, s, t, h);
+                if (L == 0.0) {                    // topology.c:1848-1852
+                    L = 1.0;
+                    f |= F_ZEROLAT;
+                }
+            }
+        }
+        tab.lat[base + j] = L;
+        tab.rel[base + j] = Rl;
+        tab.hops[base + j] = h;
+        tab.flags[base + j] = f;
+        if (tab.pred) tab.pred[base + j] = pv;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_sparse_rows
+// ---------------------------------------------------------------------------
+template <bool LDSDIST>
+__global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
+    DevGraph g, DevTable tab, DevScratch sc, const int32_t* __restrict__ rows, int32_t nRows,
+    uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Ctrl* ctl = reinterpret_cast<Ctrl*>(smem);
+    const int n = g.n;
+    const int nw = (n + 31) >> 5;
+    const int tid = threadIdx.x, NT = blockDim.x;
+    const int lane = tid & 63, wave = tid >> 6, NWV = NT >> 6;
+
+    size_t off = 64;
+    unsigned long long* ldist = reinterpret_cast<unsigned long long*>(smem + off);
+    if (LDSDIST) off += (size_t)8 * n;
+    uint32_t* pend = reinterpret_cast<uint32_t*>(smem + off);
+    off += ((size_t)4 * nw + 15) & ~(size_t)15;
+    int32_t* queue = reinterpret_cast<int32_t*>(smem + off);
+    off += (size_t)4 * qcap;
+    int32_t* heavyQ = reinterpret_cast<int32_t*>(smem + off);
+
+    const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
+    unsigned long long* dist =
+        LDSDIST ? ldist : reinterpret_cast<unsigned long long*>(sc.dist + slot);
+    int32_t* H = sc.hops + slot;
+    double* R = sc.rel + slot;
+    int32_t* P = sc.pred + slot;
+
+    for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
+        const int r = rows[b];
+        const int s = g.attached[r];
+        for (int v = tid; v < n; v += NT) dist[v] = INF_BITS;
+        for (int w = tid; w < nw; w += NT) pend[w] = 0u;
+        if (tid == 0) {
+            ctl->qtail[0] = ctl->qtail[1] = 0;
+            ctl->htail[0] = ctl->htail[1] = 0;
+            ctl->minNext[0] = ctl->minNext[1] = INF_BITS;
+            ctl->ambig = 0;
+            ctl->mismatch = 0;
+            ctl->changed = 0;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            dist[s] = d2b(0.0);
+            pend[s >> 5] = 1u << (s & 31);
+            H[s] = 0;
+            R[s] = 1.0;
+            P[s] = -1;
+        }
+        __syncthreads();
+
+        // ---------------- delta-stepping (label-correcting) ----------------
+        int par = 0;
+        double bound = delta;
+        for (;;) {
+            unsigned long long myMin = INF_BITS;
+            for (int w = tid; w < nw; w += NT) {
+                const uint32_t bits = pend[w];
+                if (!bits) continue;
+                uint32_t x = bits, taken = 0;
+                while (x) {
+                    const int bb = __ffs(x) - 1;
+                    x &= x - 1;
+                    const int v = (w << 5) + bb;
+                    const unsigned long long d = dist[v];
+                    if (b2d(d) < bound) {
+                        const int deg = g.rowPtr[v + 1] - g.rowPtr[v];
+                        if (deg >= heavyDeg) {
+                            const int pos = atomicAdd(&ctl->htail[par], 1);
+                            if (pos < hcap) { heavyQ[pos] = v; taken |= 1u << bb; }
+                        } else {
+                            const int pos = atomicAdd(&ctl->qtail[par], 1);
+                            if (pos < qcap) { queue[pos] = v; taken |= 1u << bb; }
+                        }
+                    } else {
+                        myMin = d < myMin ? d : myMin;
+                    }
+                }
+                if (taken) pend[w] = bits & ~taken;
+            }
+            myMin = wave_min_u64(myMin);
+            if (lane == 0 && myMin != INF_BITS) atomicMin(&ctl->minNext[par], myMin);
+            __syncthreads();
+            const int qn = min(ctl->qtail[par], qcap);
+            const int hn = min(ctl->htail[par], hcap);
+            const unsigned long long mn = ctl->minNext[par];
+            if (tid == 0) {
+                ctl->qtail[par ^ 1] = 0;
+                ctl->htail[par ^ 1] = 0;
+                ctl->minNext[par ^ 1] = INF_BITS;
+            }
+            if (qn == 0 && hn == 0) {
+                if (mn == INF_BITS) break;
+                const double m = b2d(mn);
+                bound = (floor(m / delta) + 1.0) * delta;
+                if (!(m < bound)) bound = m + delta;
+                par ^= 1;
+                __syncthreads();
+                continue;
+            }
+            // light vertices: one thread per vertex
+            for (int i = tid; i < qn; i += NT) {
+                const int u = queue[i];
+                const double du = b2d(ld_relaxed(&dist[u]));
+                const int hu = H[u];
+                const double ru = R[u];
+                const int a1 = g.rowPtr[u + 1];
+                for (int a = g.rowPtr[u]; a < a1; ++a) {
+                    const int v = g.col[a];
+                    const unsigned long long nb = d2b(du + g.lat[a]);
+                    if (nb < ld_relaxed(&dist[v])) {
+                        const unsigned long long old = atomicMin(&dist[v], nb);
+                        if (nb < old) {
+                            atomicOr(&pend[v >> 5], 1u << (v & 31));
+                            H[v] = hu + 1;
+                            R[v] = ru * g.rel[a];
+                        }
+                    }
+                }
+            }
+            // heavy vertices: one wave per vertex, lanes stride the arcs
+            for (int i = wave; i < hn; i += NWV) {
+                const int u = heavyQ[i];
+                const double du = b2d(ld_relaxed(&dist[u]));
+                const int hu = H[u];
+                const double ru = R[u];
+                const int a1 = g.rowPtr[u + 1];
+                for (int a = g.rowPtr[u] + lane; a < a1; a += 64) {
+                    const int v = g.col[a];
+                    const unsigned long long nb = d2b(du + g.lat[a]);
+                    if (nb < ld_relaxed(&dist[v])) {
+                        const unsigned long long old = atomicMin(&dist[v], nb);
+                        if (nb < old) {
+                            atomicOr(&pend[v >> 5], 1u << (v & 31));
+                            H[v] = hu + 1;
+                            R[v] = ru * g.rel[a];
+                        }
+                    }
+                }
+            }
+            par ^= 1;
+            __syncthreads();
+        }
+
+        // ---------------- predecessor pass + tie detector -------------------
+        // igraph sets parent[v] on the first strict improvement to the final
+        // distance, i.e. from the first POPPED tight predecessor; pops are in
+        // non-decreasing dist, so it is the tight in-arc with minimum dist[u]
+        // unless two distinct vertices tie on that minimum (then the heap's
+        // pop order decides -> row goes to k_exact_rows).
+        int myAmb = 0, myMis = 0;
+        for (int v = tid; v < n; v += NT) {
+            if (v == s) continue;
+            const unsigned long long dvb = dist[v];
+            if (dvb == INF_BITS) { P[v] = -1; continue; }
+            const double dv = b2d(dvb);
+            unsigned long long best = INF_BITS;
+            int cnt = 0, ba = -1;
+            const int a1 = g.inPtr[v + 1];
+            for (int a = g.inPtr[v]; a < a1; ++a) {
+                const int u = g.inCol[a];
+                const unsigned long long dub = dist[u];
+                if (dub > dvb) continue;
+                if (b2d(dub) + g.inLat[a] == dv) {
+                    if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
+                    if (dub < best) { best = dub; cnt = 1; ba = a; }
+                    else if (dub == best) ++cnt;
+                }
+            }
+            if (cnt != 1) { myAmb = 1; if (ba < 0) { P[v] = -1; continue; } }
+            P[v] = ba;
+            const int u = g.inCol[ba];
+            if (H[v] != H[u] + 1 || R[v] != R[u] * g.inRel[ba]) myMis = 1;
+        }
+        if (myAmb) atomicOr(&ctl->ambig, 1);
+        if (myMis) atomicOr(&ctl->mismatch, 1);
+        __syncthreads();
+        if (ctl->ambig) {
+            if (tid == 0) rowAmbig[b] = 1;
+            __syncthreads();
+            continue;
+        }
+        // Optimistic labels raced: fix by Jacobi sweeps over the tree until a
+        // sweep changes nothing (then every label satisfies its equation).
+        if (ctl->mismatch) {
+            for (;;) {
+                if (tid == 0) ctl->changed = 0;
+                __syncthreads();
+                int ch = 0;
+                for (int v = tid; v < n; v += NT) {
+                    const int a = P[v];
+                    if (v == s || a < 0) continue;
+                    const int u = g.inCol[a];
+                    const int eh = H[u] + 1;
+                    const double er = R[u] * g.inRel[a];
+                    if (H[v] != eh || R[v] != er) { H[v] = eh; R[v] = er; ch = 1; }
+                }
+                if (ch) atomicOr(&ctl->changed, 1);
+                __syncthreads();
+                if (!ctl->changed) break;
+                __syncthreads();
+            }
+        }
+        if (tid == 0) rowAmbig[b] = 0;
+        write_row(g, tab, r, s, [&](int t) { return dist[t]; }, H, R, P, 0, tid, NT);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_exact_rows: igraph 0.7.1 Dijkstra with the 2-way heap (heap.c), one wave
+// per row.  index2: 0 never reached, 1 popped, >=2 heap position + 2.
+// ---------------------------------------------------------------------------
+struct XHeap {
+    double* key;
+    int32_t* idx;
+    int32_t* index2;
+    int size;
+};
+
+__device__ __forceinline__ void xh_switch(XHeap& h, int e1, int e2) {
+    if (e1 != e2) {
+        const double t3 = h.key[e1];
+        h.key[e1] = h.key[e2];
+        h.key[e2] = t3;
+        const int t1 = h.idx[e1], t2 = h.idx[e2];
+        h.index2[t1] = e2 + 2;
+        h.index2[t2] = e1 + 2;
+        h.idx[e1] = t2;
+        h.idx[e2] = t1;
+    }
+}
+
+__device__ void xh_shift_up(XHeap& h, int elem) {
+    while (!(elem == 0 || h.key[elem] < h.key[((elem + 1) >> 1) - 1])) {
+        const int p = ((elem + 1) >> 1) - 1;
+        xh_switch(h, elem, p);
+        elem = p;
+    }
+}
+
+__device__ void xh_sink(XHeap& h, int head) {
+    for (;;) {
+        const int l = (head + 1) * 2 - 1, rr = (head + 1) * 2;
+        if (l >= h.size) return;
+        if (rr == h.size || h.key[l] >= h.key[rr]) {
+            if (h.key[head] < h.key[l]) { xh_switch(h, head, l); head = l; }
+            else return;
+        } else {
+            if (h.key[head] < h.key[rr]) { xh_switch(h, head, rr); head = rr; }
+            else return;
+        }
+    }
+}
+
+__device__ __forceinline__ void xh_push(XHeap& h, int v, double k) {
+    const int sz = h.size;
+    h.key[sz] = k;
+    h.idx[sz] = v;
+    h.size = sz + 1;
+    h.index2[v] = sz + 2;
+    xh_shift_up(h, sz);
+}
+
+__device__ __forceinline__ void xh_modify(XHeap& h, int v, double k) {
+    const int pos = h.index2[v] - 2;
+    h.key[pos] = k;
+    xh_sink(h, pos);
+    xh_shift_up(h, pos);
+}
+
+template <bool LDSIDX>
+__global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g, DevTable tab, DevScratch sc,
+                                                           const int32_t* __restrict__ rows,
+                                                           int32_t nRows) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int n = g.n;
+    const int lane = threadIdx.x;
+    const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
+    int32_t* index2 = LDSIDX ? reinterpret_cast<int32_t*>(smem) : sc.index2 + slot;
+    double* D = sc.dist + slot;
+    int32_t* H = sc.hops + slot;
+    double* R = sc.rel + slot;
+    int32_t* P = sc.pred + slot;
+
+    for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
+        const int r = rows[b];
+        const int s = g.attached[r];
+        for (int v = lane; v < n; v += EX_THREADS) index2[v] = 0;
+        __syncthreads();
+        XHeap h{sc.heapKey + slot, sc.heapIdx + slot, index2, 0};
+        if (lane == 0) {
+            xh_push(h, s, 0.0);
+            H[s] = 0;
+            R[s] = 1.0;
+            P[s] = -1;
+        }
+        int toReach = g.T;
+        int hsize = 1;
+        while (hsize > 0 && toReach > 0) {
+            int u = 0;
+            double mind = 0.0;
+            if (lane == 0) {
+                u = h.idx[0];
+                const double k = h.key[0];
+                xh_switch(h, 0, h.size - 1);
+                h.size -= 1;
+                h.index2[u] = 1;
+                xh_sink(h, 0);
+                mind = -k;
+                D[u] = mind;
+            }
+            u = __shfl(u, 0, 64);
+            mind = __shfl(mind, 0, 64);
+            if (g.isAttached[u]) --toReach;
+            const int hu = H[u];
+            const double ru = R[u];
+            const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
+            for (int base = a0; base < a1; base += 64) {
+                const int a = base + lane;
+                int myV = -1, myIn = -1;
+                double myW = 0.0, myR = 0.0;
+                if (a < a1) { myV = g.col[a]; myW = g.lat[a]; myR = g.rel[a]; myIn = g.outToIn[a]; }
+                const int cnt = min(64, a1 - base);
+                for (int k = 0; k < cnt; ++k) {
+                    const int v = __shfl(myV, k, 64);
+                    const double w = __shfl(myW, k, 64);
+                    const double rw = __shfl(myR, k, 64);
+                    const int ia = __shfl(myIn, k, 64);
+                    if (lane == 0) {
+                        const double alt = mind + w;
+                        const int st = h.index2[v];
+                        if (st == 0) {
+                            xh_push(h, v, -alt);
+                            P[v] = ia; H[v] = hu + 1; R[v] = ru * rw;
+                        } else if (st >= 2) {
+                            const double cur = -h.key[st - 2];
+                            if (alt < cur) {
+                                xh_modify(h, v, -alt);
+                                P[v] = ia; H[v] = hu + 1; R[v] = ru * rw;
+                            }
+                        }
+                    }
+                }
+            }
+            hsize = __shfl(h.size, 0, 64);
+        }
+        __syncthreads();
+        write_row(g, tab, r, s,
+                  [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
+                  H, R, P, F_EXACT, lane, EX_THREADS);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_direct_rows: complete graphs (and prefersDirectPaths pairs): row entry =
+// _topology_lookupDirectPath (topology.c:1877-1927).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_direct_rows(DevGraph g, DevTable tab,
+                                                     const int32_t* __restrict__ rows) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    const int r = rows[blockIdx.y];
+    if (j >= g.T) return;
+    const int s = g.attached[r];
+    const int t = g.attached[j];
+    double acc = 1.0 * g.vrel[s];
+    acc = acc * g.vrel[t];
+    double L = 0.0, Rl = acc;
+    int h = -1;
+    uint8_t f = F_DIRECT;
+    if (t == s) {
+        if (g.hasSelf[s]) { L = 0.0 + g.selfLat[s]; Rl = acc * g.selfRel[s]; h = 1; }
+        else f |= F_NOEDGE;
+    } else {
+        const int a0 = g.rowPtr[s], a1 = g.rowPtr[s + 1];
+        int a = -1;
+        if (a1 - a0 == g.n - 1) {
+            a = a0 + (t < s ? t : t - 1);
+        } else {
+            int lo = a0, hi = a1;
+            while (lo < hi) {
+                const int mid = lo + ((hi - lo) >> 1);
+                if (g.col[mid] < t) lo = mid + 1; else hi = mid;
+            }
+            if (lo < a1 && g.col[lo] == t) a = lo;
+        }
+        if (a >= 0) { L = 0.0 + g.lat[a]; Rl = acc * g.rel[a]; h = 1; }
+        else f |= F_NOEDGE;
+    }
+    const size_t idx = (size_t)r * (size_t)tab.T + j;
+    tab.lat[idx] = L;
+    tab.rel[idx] = Rl;
+    tab.hops[idx] = h;
+    tab.flags[idx] = f;
+    if (tab.pred) tab.pred[idx] = (t == s) ? -1 : s;
+}
+
+// ---------------------------------------------------------------------------
+int sparse_max_threads() { return SP_THREADS; }
+
+void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                        const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
+                        const SparseLaunch& cfg, void* stream) {
+    if (nRows <= 0) return;
+    const int grid = nRows < cfg.grid ? nRows : cfg.grid;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (cfg.ldsDist) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
+        hipLaunchKernelGGL(k_sparse_rows<true>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st,
+                           g, tab, sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap,
+                           cfg.heavyDeg);
+    } else {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
+        hipLaunchKernelGGL(k_sparse_rows<false>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st,
+                           g, tab, sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap,
+                           cfg.heavyDeg);
+    }
+}
+
+void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                       const int32_t* dRows, int32_t nRows, int32_t grid, bool ldsIndex,
+                       void* stream) {
+    if (nRows <= 0) return;
+    if (grid > nRows) grid = nRows;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (ldsIndex) {
+        const int bytes = (int)(((size_t)4 * g.n + 15) & ~(size_t)15);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipLaunchKernelGGL(k_exact_rows<true>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab,
+                           sc, dRows, nRows);
+    } else {
+        hipLaunchKernelGGL(k_exact_rows<false>, dim3(grid), dim3(EX_THREADS), 0, st, g, tab, sc,
+                           dRows, nRows);
+    }
+}
+
+void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
+                        int32_t nRows, void* stream) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int bx = (g.T + 255) / 256;
+    for (int r0 = 0; r0 < nRows; r0 += 65535) {
+        const int cnt = (nRows - r0) < 65535 ? (nRows - r0) : 65535;
+        hipLaunchKernelGGL(k_direct_rows, dim3(bx, cnt), dim3(256), 0, st, g, tab, dRows + r0);
+    }
+}
+
+}  // namespace shdpe

@@ -1,0 +1,261 @@
+"""ctypes binding of libshdpe.so (include/shd_pathengine.h).
+
+This is plumbing for tests and bench.py: every entry point goes straight to
+the C-ABI library built from shadow-1_amd/csrc (HIP kernels for gfx950).
+There is no Python/CPU compute path -- if the library or a gfx950 device is
+missing, loading / creating the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # shadow-1_amd/
+LIB_PATH = os.path.join(_PKG, "libshdpe.so")
+
+OK, EINVAL, ENOMEM, ENODEV, EUNREACHABLE, ENOSELFLOOP, EMULTI, EHIP, ENOTATTACHED, ENOEDGE = (
+    0, -1, -2, -3, -4, -5, -6, -7, -8, -9)
+F_UNREACHABLE, F_NOEDGE, F_ZEROLAT, F_DIRECT, F_EXACT = 0x01, 0x02, 0x04, 0x08, 0x10
+F_FAILED = F_UNREACHABLE | F_NOEDGE
+
+EXPORTS = [
+    "shd_pe_default_options", "shd_pe_create", "shd_pe_destroy", "shd_pe_strerror",
+    "shd_pe_is_complete", "shd_pe_num_attached", "shd_pe_attached", "shd_pe_compute_all",
+    "shd_pe_compute_rows", "shd_pe_compute_positions", "shd_pe_get_row",
+    "shd_pe_copy_rows_device", "shd_pe_synchronize", "shd_pe_get_stats", "shd_pe_reset_stats",
+    "shd_pe_direct_path", "shd_pe_self_path", "shd_pe_adjacent", "shd_topology_new",
+    "shd_topology_free", "shd_topology_get_latency", "shd_topology_get_reliability",
+    "shd_topology_is_routable", "shd_topology_increment_path_packet_counter",
+    "shd_topology_cached", "shd_topology_min_latency", "shd_topology_cache_size",
+    "shd_topology_rows_computed",
+]
+
+
+class GraphDesc(C.Structure):
+    _fields_ = [("nVertices", C.c_int32), ("nEdges", C.c_int64), ("directed", C.c_int32),
+                ("edgeFrom", C.c_void_p), ("edgeTo", C.c_void_p), ("edgeLatency", C.c_void_p),
+                ("edgePacketLoss", C.c_void_p), ("vertexPacketLoss", C.c_void_p)]
+
+
+class Options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("batchRows", C.c_int32), ("delta", C.c_double),
+                ("storePred", C.c_int32), ("forceMode", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("rowsComputed", C.c_int64), ("rowsExact", C.c_int64),
+                ("arcsRelaxed", C.c_int64), ("msSparseKernel", C.c_double),
+                ("msExactKernel", C.c_double), ("msDirectKernel", C.c_double),
+                ("msTotal", C.c_double), ("launchesSparse", C.c_int64),
+                ("launchesExact", C.c_int64), ("launchesDirect", C.c_int64),
+                ("mode", C.c_int32), ("isComplete", C.c_int32), ("nVertices", C.c_int32),
+                ("nArcs", C.c_int64), ("nAttached", C.c_int32), ("deltaUsed", C.c_double)]
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what}: {strerror(code)} ({code})")
+        self.code = code
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libshdpe.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libshdpe.so not built at {path}: run "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C shadow-1_amd)")
+    lib = C.CDLL(path)
+    vp, i32, i64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    sig = {
+        "shd_pe_default_options": (None, [vp]),
+        "shd_pe_create": (C.c_int, [vp, vp, i32, vp, vp]),
+        "shd_pe_destroy": (None, [vp]),
+        "shd_pe_strerror": (C.c_char_p, [C.c_int]),
+        "shd_pe_is_complete": (C.c_int, [vp]),
+        "shd_pe_num_attached": (i32, [vp]),
+        "shd_pe_attached": (C.c_int, [vp, vp]),
+        "shd_pe_compute_all": (C.c_int, [vp]),
+        "shd_pe_compute_rows": (C.c_int, [vp, vp, i32]),
+        "shd_pe_compute_positions": (C.c_int, [vp, i32, i32]),
+        "shd_pe_get_row": (C.c_int, [vp, i32, vp, vp, vp, vp, vp]),
+        "shd_pe_copy_rows_device": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
+        "shd_pe_synchronize": (C.c_int, [vp]),
+        "shd_pe_get_stats": (C.c_int, [vp, vp]),
+        "shd_pe_reset_stats": (C.c_int, [vp]),
+        "shd_pe_direct_path": (C.c_int, [vp, i32, i32, vp, vp]),
+        "shd_pe_self_path": (C.c_int, [vp, i32, vp, vp]),
+        "shd_pe_adjacent": (C.c_int, [vp, i32, i32]),
+        "shd_topology_new": (C.c_int, [vp, i32, vp]),
+        "shd_topology_free": (None, [vp]),
+        "shd_topology_get_latency": (f64, [vp, i32, i32]),
+        "shd_topology_get_reliability": (f64, [vp, i32, i32]),
+        "shd_topology_is_routable": (C.c_int, [vp, i32, i32]),
+        "shd_topology_increment_path_packet_counter": (C.c_int, [vp, i32, i32]),
+        "shd_topology_cached": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
+        "shd_topology_min_latency": (f64, [vp]),
+        "shd_topology_cache_size": (i64, [vp]),
+        "shd_topology_rows_computed": (i64, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def strerror(code: int) -> str:
+    return load_library().shd_pe_strerror(int(code)).decode()
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Engine:
+    """One path engine on one gfx950 device (shd_pe_create)."""
+
+    def __init__(self, top, attached, device: int = 0, delta: float = 0.0,
+                 store_pred: bool = True, force_mode: int = 0):
+        lib = load_library()
+        self._lib = lib
+        self.top = top
+        self._arrays = [top.src, top.dst, top.latency, top.loss, top.vloss]
+        d = GraphDesc(top.n, top.m, int(top.directed), _p(top.src), _p(top.dst),
+                      _p(top.latency), _p(top.loss), _p(top.vloss))
+        o = Options()
+        lib.shd_pe_default_options(C.byref(o))
+        o.device, o.delta, o.storePred, o.forceMode = device, delta, int(store_pred), force_mode
+        att = np.ascontiguousarray(attached, dtype=np.int32)
+        h = C.c_void_p()
+        rc = lib.shd_pe_create(C.byref(d), _p(att), att.shape[0], C.byref(o), C.byref(h))
+        if rc:
+            raise EngineError(rc, "shd_pe_create")
+        self.h = h
+        self.store_pred = store_pred
+        T = lib.shd_pe_num_attached(h)
+        self.attached = np.empty(T, np.int32)
+        lib.shd_pe_attached(h, _p(self.attached))
+        self.T = T
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.shd_pe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _chk(self, rc, what):
+        if rc:
+            raise EngineError(rc, what)
+
+    @property
+    def is_complete(self) -> bool:
+        return bool(self._lib.shd_pe_is_complete(self.h))
+
+    def compute_all(self):
+        self._chk(self._lib.shd_pe_compute_all(self.h), "shd_pe_compute_all")
+
+    def compute_rows(self, sources):
+        s = np.ascontiguousarray(sources, dtype=np.int32)
+        self._chk(self._lib.shd_pe_compute_rows(self.h, _p(s), s.shape[0]), "shd_pe_compute_rows")
+
+    def compute_positions(self, start: int, count: int):
+        self._chk(self._lib.shd_pe_compute_positions(self.h, int(start), int(count)),
+                  "shd_pe_compute_positions")
+
+    def synchronize(self):
+        self._chk(self._lib.shd_pe_synchronize(self.h), "shd_pe_synchronize")
+
+    def get_row(self, src: int):
+        T = self.T
+        lat = np.empty(T); rel = np.empty(T)
+        hops = np.empty(T, np.int32); flags = np.empty(T, np.uint8)
+        pred = np.empty(T, np.int32) if self.store_pred else None
+        self._chk(self._lib.shd_pe_get_row(self.h, int(src), _p(lat), _p(rel), _p(hops),
+                                           _p(pred), _p(flags)), "shd_pe_get_row")
+        return dict(lat=lat, rel=rel, hops=hops, pred=pred, flags=flags)
+
+    def copy_rows_device(self, start, count, d_lat=0, d_rel=0, d_hops=0, d_flags=0):
+        self._chk(self._lib.shd_pe_copy_rows_device(
+            self.h, int(start), int(count), d_lat or None, d_rel or None, d_hops or None,
+            d_flags or None), "shd_pe_copy_rows_device")
+
+    def stats(self) -> dict:
+        s = Stats()
+        self._chk(self._lib.shd_pe_get_stats(self.h, C.byref(s)), "shd_pe_get_stats")
+        return {f: getattr(s, f) for f, _ in Stats._fields_}
+
+    def reset_stats(self):
+        self._chk(self._lib.shd_pe_reset_stats(self.h), "shd_pe_reset_stats")
+
+    def direct_path(self, s, t):
+        lat, rel = C.c_double(), C.c_double()
+        rc = self._lib.shd_pe_direct_path(self.h, int(s), int(t), C.byref(lat), C.byref(rel))
+        return None if rc else (lat.value, rel.value)
+
+    def self_path(self, v):
+        lat, rel = C.c_double(), C.c_double()
+        rc = self._lib.shd_pe_self_path(self.h, int(v), C.byref(lat), C.byref(rel))
+        return None if rc else (lat.value, rel.value)
+
+
+class TopologyShim:
+    """topology_getLatency/getReliability/isRoutable/incrementPathPacketCounter
+    (topology.c:2053-2092) over the engine (shd_topology_*)."""
+
+    def __init__(self, engine: Engine, prefers_direct: bool = False):
+        self.engine = engine
+        self._lib = engine._lib
+        h = C.c_void_p()
+        rc = self._lib.shd_topology_new(engine.h, int(prefers_direct), C.byref(h))
+        if rc:
+            raise EngineError(rc, "shd_topology_new")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.shd_topology_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def get_latency(self, s, d):
+        return self._lib.shd_topology_get_latency(self.h, int(s), int(d))
+
+    def get_reliability(self, s, d):
+        return self._lib.shd_topology_get_reliability(self.h, int(s), int(d))
+
+    def is_routable(self, s, d):
+        return bool(self._lib.shd_topology_is_routable(self.h, int(s), int(d)))
+
+    def increment(self, s, d):
+        return self._lib.shd_topology_increment_path_packet_counter(self.h, int(s), int(d))
+
+    def cached(self, s, d):
+        lat, rel = C.c_double(), C.c_double()
+        isd, pc = C.c_int32(), C.c_int64()
+        ok = self._lib.shd_topology_cached(self.h, int(s), int(d), C.byref(lat), C.byref(rel),
+                                           C.byref(isd), C.byref(pc))
+        return (lat.value, rel.value, bool(isd.value), pc.value) if ok else None
+
+    @property
+    def min_latency(self):
+        return self._lib.shd_topology_min_latency(self.h)
+
+    @property
+    def cache_size(self):
+        return self._lib.shd_topology_cache_size(self.h)
+
+    @property
+    def rows_computed(self):
+        return self._lib.shd_topology_rows_computed(self.h)
