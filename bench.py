@@ -1,0 +1,196 @@
+"""Benchmark: path-table construction (source rows/sec), BASELINE.json metric.
+
+python bench.py --gpus N --steps K --warmup W [--workload c2] [--allgather]
+
+A step = one full path-table construction for the workload (all S source
+rows, S = T = attached vertices), sharded over the N ranks in contiguous
+blocks of rows (strong scaling: the table is fixed, ranks split it).  Each
+rank owns one engine on its own GPU (libshdpe.so, HIP kernels); no exchange
+on the data path.  --allgather additionally assembles the whole table on
+every rank with an RCCL all-gather over xGMI (reported separately).
+
+Inputs (graph, attached set) are uploaded before the timed region; rows stay
+in HBM (the D2H to the host path cache is outside `value`).
+
+rank 0 prints ONE JSON line.  cpu_baseline = the oracle (C restatement of
+igraph 0.7.1 Dijkstra + topology.c fold) on 1 host thread, on a bounded
+sample of the same rows (the reference serialises all Dijkstra runs under
+graphLock, topology.c:1747-1781).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "shadow-1_amd"), os.path.join(ROOT, "oracle")]
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_row(n, m_arcs, T):
+    """SURVEY.md §8(d) frozen formula for a sparse row: 12*m_arcs + 12*n + 20*T."""
+    return 12 * m_arcs + 12 * n + 20 * T
+
+
+def shard(T, rank, world):
+    start = (T * rank) // world
+    end = (T * (rank + 1)) // world
+    return start, end - start
+
+
+def cpu_baseline(top, att, budget_s=12.0, max_rows=4000):
+    """Time the oracle on a bounded sample of the workload's rows (1 thread)."""
+    import oracle as O
+    O.build()
+    og = O.OracleGraph(top)
+    rng = np.random.default_rng(0)
+    order = rng.permutation(att.shape[0])
+    done, t0 = 0, time.perf_counter()
+    chunk = 16
+    while done < max_rows and time.perf_counter() - t0 < budget_s:
+        srcs = att[order[done:done + chunk]]
+        og.rows(srcs, att, threads=1)
+        done += srcs.shape[0]
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "source rows/s", "cores": 1, "kind": "port",
+            "sample": f"{done} random source rows of the same workload (all {att.shape[0]} "
+                      f"targets each), igraph-0.7.1-faithful 2-wheap Dijkstra + "
+                      f"_topology_computePathProperties fold, 1 thread, {dt:.1f} s"}
+
+
+def load_traffic(workload):
+    p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from shdpe import generators as G
+    from shdpe.engine import Engine
+
+    top, att = G.make_config(args.workload)
+    eng = Engine(top, att, device=local)
+    T = eng.T
+    start, count = shard(T, rank, world)
+    st0 = eng.stats()
+    n, m_arcs = st0["nVertices"], st0["nArcs"]
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+        eng.synchronize()
+
+    for _ in range(args.warmup):
+        eng.compute_positions(start, count)
+    barrier_sync()
+    eng.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.compute_positions(start, count)
+    eng.synchronize()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    st = eng.stats()
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    gather = None
+    if args.allgather and dist is not None:
+        import torch
+        # equal-size blocks for the collective (pad the last shard)
+        blk = (T + world - 1) // world
+        mine = torch.zeros(blk * T, dtype=torch.float64, device=f"cuda:{local}")
+        eng.copy_rows_device(start, count, d_lat=mine.data_ptr())
+        full = torch.empty(world * blk * T, dtype=torch.float64, device=f"cuda:{local}")
+        torch.cuda.synchronize(); dist.barrier()
+        g0 = time.perf_counter()
+        dist.all_gather_into_tensor(full, mine)
+        torch.cuda.synchronize()
+        g1 = time.perf_counter()
+        gather = {"bytes_per_rank": mine.numel() * 8, "ms": (g1 - g0) * 1e3,
+                  "field": "latency f64"}
+
+    rows_total = T * args.steps
+    value = rows_total / elapsed
+    ms_kernel = st["msSparseKernel"] + st["msDirectKernel"]
+    launches = max(1, st["launchesSparse"] + st["launchesDirect"])
+    avg_launch_ms = ms_kernel / launches
+    if st["mode"] == 2:
+        bytes_per_launch = 36 * T * count
+        kname = "k_direct_rows"
+    else:
+        bytes_per_launch = algorithmic_bytes_per_row(n, m_arcs, T) * count
+        kname = "k_sparse_rows"
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.workload)
+    out = {
+        "metric": "path-table source rows/sec (latency+reliability)",
+        "value": value,
+        "unit": "source rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": args.workload, "vertices": n, "arcs": m_arcs,
+                   "sources": T, "targets": T, "rows_per_step": T,
+                   "parallelism": f"source-row shards x{world}"},
+        "edges_relaxed_per_s": m_arcs * rows_total / elapsed,
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": (traffic or {}).get("bytes_per_launch"),
+                     "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "avg_launch_ms": avg_launch_ms, "launches": launches},
+        "rows_exact": st["rowsExact"] // max(1, args.steps),
+        "ms_exact_per_step": st["msExactKernel"] / max(1, args.steps),
+    }
+    if gather:
+        out["allgather"] = gather
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(top, att, budget_s=args.cpu_budget)
+        out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+    eng.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

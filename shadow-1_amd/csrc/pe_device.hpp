@@ -71,14 +71,14 @@ struct SparseLaunch {
     int32_t qcap;        // light frontier queue capacity
     int32_t hcap;        // heavy (wave-per-vertex) queue capacity
     int32_t heavyDeg;    // degree threshold for the heavy queue
-    bool ldsDist;        // dist array in LDS (n small enough)
+    int32_t layout;      // 2: dist+hops+rowPtr in LDS, 1: dist in LDS, 0: HBM slot
     double delta;        // bucket width
 };
 
 // kernels (pe_kernels.hip); all launched on `stream`.
 void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
-                        const SparseLaunch& cfg, void* stream);
+                        const SparseLaunch& cfg, int32_t* dDbg, void* stream);
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, bool ldsIndex,
                        void* stream);

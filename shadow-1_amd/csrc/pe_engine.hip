@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -36,6 +37,7 @@ struct ShdPe {
     bool tableReady = false;
     int32_t* dRows = nullptr;
     uint8_t* dRowAmbig = nullptr;
+    int32_t* dDbg = nullptr;          // per-row kernel counters (SHDPE_DEBUG=1)
     int32_t rowsCap = 0;
     SparseLaunch cfg{};
     int exactGrid = 0;
@@ -103,31 +105,44 @@ extern "C" const char* shd_pe_strerror(int code) {
     }
 }
 
+static inline int a16(long x) { return (int)((x + 15) & ~15L); }
+
 static void configure(ShdPe* pe) {
     const HostGraph& g = pe->hg;
-    const int n = g.n;
-    const int nw = (n + 31) / 32;
+    const long n = g.n;
+    const long nw = (n + 31) / 32;
     const int LDS = 160 * 1024;
     SparseLaunch c{};
-    c.threads = env_int("SHDPE_THREADS", 512);
+    c.threads = env_int("SHDPE_THREADS", 1024);
     if (c.threads > sparse_max_threads()) c.threads = sparse_max_threads();
     c.hcap = 256;
     c.heavyDeg = env_int("SHDPE_HEAVY_DEG", 64);
-    const int fixedPend = 64 + ((4 * nw + 15) & ~15) + 4 * c.hcap;
-    const int qmin = 4096;
-    c.ldsDist = (fixedPend + 8 * n + 4 * qmin) <= LDS && env_int("SHDPE_NO_LDS_DIST", 0) == 0;
-    int room = LDS - fixedPend - (c.ldsDist ? 8 * n : 0);
-    c.qcap = std::min(room / 4, std::max(n, 1024));
-    if (c.qcap < 256) c.qcap = 256;
-    c.ldsBytes = fixedPend + (c.ldsDist ? 8 * n : 0) + 4 * c.qcap;
-    int wgPerCU = std::max(1, std::min(4, LDS / std::max(c.ldsBytes, 1)));
+    const int qmin = 2048;
+    const int base = 64 + 2 * a16(4 * nw) + a16(4 * c.hcap);
+    const int need2 = base + a16(8 * n) + a16(2 * n) + a16(4 * (n + 1));
+    const int need1 = base + a16(8 * n);
+    int layout = 0, used = base;
+    if (need2 + 4 * qmin <= LDS) { layout = 2; used = need2; }
+    else if (need1 + 4 * qmin <= LDS) { layout = 1; used = need1; }
+    const int forced = env_int("SHDPE_LAYOUT", -1);
+    if (forced >= 0 && forced < layout) {
+        layout = forced;
+        used = forced == 1 ? need1 : base;
+    }
+    c.layout = layout;
+    c.qcap = (int)std::min<long>((LDS - used) / 4, std::max<long>(n, 1024));
+    c.qcap &= ~3;
+    c.ldsBytes = used + 4 * c.qcap;
+    const int maxWG = env_int("SHDPE_WG_PER_CU", 8);
+    const int wgPerCU = std::max(1, std::min({maxWG, LDS / std::max(c.ldsBytes, 1),
+                                              2048 / c.threads}));
     c.grid = pe->numCUs * wgPerCU;
-    double factor = env_double("SHDPE_DELTA_FACTOR", 4.0);
+    const double factor = env_double("SHDPE_DELTA_FACTOR", 16.0);
     c.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * factor;
     if (!(c.delta > 0)) c.delta = 1.0;
     pe->cfg = c;
     pe->exactLdsIdx = (size_t)4 * n <= 64 * 1024;
-    int exPerCU = pe->exactLdsIdx ? std::max(1, std::min(8, LDS / std::max(4 * n, 1))) : 8;
+    int exPerCU = pe->exactLdsIdx ? std::max(1, std::min(8, LDS / std::max<int>(4 * n, 1))) : 8;
     pe->exactGrid = pe->numCUs * exPerCU;
     pe->stats.deltaUsed = c.delta;
 }
@@ -259,6 +274,11 @@ static int ensure_table(ShdPe* pe) {
         return rc;
     pe->dRows = (int32_t*)rows;
     pe->dRowAmbig = (uint8_t*)amb;
+    if (env_int("SHDPE_DEBUG", 0)) {
+        void* dbg;
+        if ((rc = dev_alloc(pe, &dbg, (size_t)pe->rowsCap * 32))) return rc;
+        pe->dDbg = (int32_t*)dbg;
+    }
     pe->tableReady = true;
     return SHD_PE_OK;
 }
@@ -296,7 +316,7 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
         } else {
             HIPCHK(hipEventRecord(pe->evA, pe->stream));
             launch_sparse_rows(pe->dg, pe->tab, pe->sc, pe->dRows, cnt, pe->dRowAmbig, pe->cfg,
-                               pe->stream);
+                               pe->dDbg, pe->stream);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(pe->evB, pe->stream));
             amb.resize(cnt);
@@ -307,6 +327,25 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
             pe->stats.launchesSparse++;
             for (int32_t i = 0; i < cnt; ++i)
                 if (amb[i]) exactRows.push_back(pos[c0 + i]);
+            if (pe->dDbg) {
+                std::vector<int32_t> dbg((size_t)cnt * 8);
+                HIPCHK(hipMemcpy(dbg.data(), pe->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
+                double ph = 0, cy[4] = {0, 0, 0, 0};
+                int phMax = 0, jMax = 0, mis = 0, am = 0; long jSum = 0;
+                for (int32_t i = 0; i < cnt; ++i) {
+                    ph += dbg[8 * i]; phMax = std::max(phMax, dbg[8 * i]);
+                    jMax = std::max(jMax, dbg[8 * i + 1]); jSum += dbg[8 * i + 1];
+                    mis += dbg[8 * i + 2] != 0; am += dbg[8 * i + 3] != 0;
+                    for (int k = 0; k < 4; ++k) cy[k] += 16.0 * dbg[8 * i + 4 + k];
+                }
+                std::fprintf(stderr,
+                             "[shdpe] sparse rows=%d phases mean=%.1f max=%d | mismatch rows=%d "
+                             "jacobi rounds sum=%ld max=%d | ambiguous rows=%d | delta=%.3f | "
+                             "kcycles/row scan=%.1f relax=%.1f final=%.1f write=%.1f\n",
+                             cnt, ph / cnt, phMax, mis, jSum, jMax, am, pe->cfg.delta,
+                             cy[0] / cnt / 1e3, cy[1] / cnt / 1e3, cy[2] / cnt / 1e3,
+                             cy[3] / cnt / 1e3);
+            }
         }
         if (!exactRows.empty()) {
             HIPCHK(hipMemcpyAsync(pe->dRows, exactRows.data(), exactRows.size() * 4,

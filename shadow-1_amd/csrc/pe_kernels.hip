@@ -24,12 +24,14 @@
 //   k_direct_rows  complete graphs: direct-edge gather (HBM-bound).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "pe_device.hpp"
 
 namespace shdpe {
 
 constexpr unsigned long long INF_BITS = 0x7FF0000000000000ull;
-constexpr int SP_THREADS = 512;
+constexpr int SP_THREADS = 1024;
 constexpr int EX_THREADS = 64;
 
 __device__ __forceinline__ double b2d(unsigned long long b) {
@@ -92,87 +94,228 @@ __device__ __noinline__ double fold_rel_general(const DevGraph& g, const int32_t
 }
 
 // Row writer shared by the sparse and exact kernels (topology.c:1805-1864).
-template <class DistOf>
+// Targets are processed in groups of 4 so their independent loads overlap.
+template <class DistOf, class HopOf>
 __device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab, int r, int s,
-                                         DistOf distOf, const int32_t* H, const double* R,
+                                         DistOf distOf, HopOf hopOf, const double* R,
                                          const int32_t* P, uint8_t extra, int tid, int NT) {
-    const int64_t T = tab.T;
-    const size_t base = (size_t)r * (size_t)T;
-    for (int j = tid; j < T; j += NT) {
-        const int t = g.attached[j];
-        double L = 0.0, Rl = 0.0;
-        int h = -1, pv = -1;
-        uint8_t f = extra;
-        if (t == s) {
-            // 1-vertex igraph path [s]: the fold uses edge (s,s) (:1469-1488),
-            // the destination factor is skipped (:1457).
-            if (g.hasSelf[s]) {
-                L = 0.0 + g.selfLat[s];
-                Rl = (1.0 * g.vrel[s]) * g.selfRel[s];
-                h = 1;
-            } else {
-                f |= F_NOEDGE;
-            }
-        } else {
-            const unsigned long long db = distOf(t);
-            if (db == INF_BITS) {
+    const int T = (int)tab.T;
+    const size_t base = (size_t)r * (size_t)tab.T;
+    double* __restrict__ oLat = tab.lat + base;
+    double* __restrict__ oRel = tab.rel + base;
+    int32_t* __restrict__ oHops = tab.hops + base;
+    uint8_t* __restrict__ oFlags = tab.flags + base;
+    int32_t* __restrict__ oPred = tab.pred ? tab.pred + base : nullptr;
+    constexpr int G = 4;
+    for (int j0 = tid; j0 < T; j0 += NT * G) {
+        int tt[G], pa[G], hh[G];
+        unsigned long long db[G];
+        double rr[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int j = j0 + k * NT;
+            tt[k] = j < T ? g.attached[j] : s;
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int t = tt[k];
+            db[k] = distOf(t);
+            if (t != s && db[k] != INF_BITS) { hh[k] = hopOf(t); rr[k] = R[t]; pa[k] = P[t]; }
+            else { hh[k] = -1; rr[k] = 0.0; pa[k] = -1; }
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int j = j0 + k * NT;
+            if (j >= T) continue;
+            const int t = tt[k];
+            double L = 0.0, Rl = 0.0;
+            int h = -1, pv = -1;
+            uint8_t f = extra;
+            if (t == s) {
+                // 1-vertex igraph path [s]: the fold uses edge (s,s) (:1469-1488),
+                // the destination factor is skipped (:1457).
+                if (g.hasSelf[s]) {
+                    L = 0.0 + g.selfLat[s];
+                    Rl = (1.0 * g.vrel[s]) * g.selfRel[s];
+                    h = 1;
+                } else {
+                    f |= F_NOEDGE;
+                }
+            } else if (db[k] == INF_BITS) {
                 f |= F_UNREACHABLE;
             } else {
-                L = b2d(db);
-                h = H[t];
-                const int pa = P[t];
-                pv = g.inCol[pa];
-                if (g.vrel[s] == 1.0 && g.vrel[t] == 1.0) Rl = R[t];
+                L = b2d(db[k]);
+                h = hh[k];
+                if (oPred) pv = g.inCol[pa[k]];
+                if (g.vrel[s] == 1.0 && g.vrel[t] == 1.0) Rl = rr[k];
                 else Rl = fold_rel_general(g, P, s, t, h);
                 if (L == 0.0) {                    // topology.c:1848-1852
                     L = 1.0;
                     f |= F_ZEROLAT;
                 }
             }
+            oLat[j] = L;
+            oRel[j] = Rl;
+            oHops[j] = h;
+            oFlags[j] = f;
+            if (oPred) oPred[j] = pv;
         }
-        tab.lat[base + j] = L;
-        tab.rel[base + j] = Rl;
-        tab.hops[base + j] = h;
-        tab.flags[base + j] = f;
-        if (tab.pred) tab.pred[base + j] = pv;
+    }
+}
+
+constexpr int UNR = 8;   // arcs loaded per batch (independent loads in flight)
+
+// Per-row state placement.  LAYOUT 2: dist, hops (u16), rowPtr in LDS;
+// LAYOUT 1: dist in LDS; LAYOUT 0: everything in the workgroup's HBM slot.
+template <int LAYOUT>
+struct RowCtx {
+    using HopT = typename std::conditional<LAYOUT == 2, uint16_t, int32_t>::type;
+    unsigned long long* dist;
+    HopT* H;
+    const int32_t* rp;
+    double* R;
+    int32_t* P;
+    uint32_t* pend;
+};
+
+// Process one frontier vertex u: (1) pull -- find the tight in-arc with the
+// minimum dist[x] under the CURRENT distances and set u's labels (hops, rel
+// product) from it; (2) push -- relax u's out-arcs with dist[u] + w
+// (ds_min_rtn_u64 on the f64 bit pattern) and mark improved vertices pending.
+// Labels are written only by the thread (or wave) processing u, so they are
+// race-free within a phase; the final pass re-verifies every label anyway.
+// W = 1: one thread per vertex; W = 64: one wave per vertex (hubs).
+template <int W, int LAYOUT>
+__device__ __forceinline__ void process_vertex(const DevGraph& g, const RowCtx<LAYOUT>& c, int u,
+                                               int s, int lane) {
+    const unsigned long long dub = ld_relaxed(&c.dist[u]);
+    const double du = b2d(dub);
+    const bool undirected = g.inCol == g.col;
+    unsigned long long best = INF_BITS;
+    int cnt = 0, ba = -1, bx = -1;
+    const int a0 = c.rp[u], a1 = c.rp[u + 1];
+    for (int a = a0 + lane * UNR; a < a1; a += W * UNR) {
+        int cv[UNR];
+        double lw[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k)
+            if (a + k < a1) { cv[k] = g.col[a + k]; lw[k] = g.lat[a + k]; }
+        unsigned long long dx[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) dx[k] = (a + k < a1) ? ld_relaxed(&c.dist[cv[k]]) : 0ull;
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            if (a + k < a1) {
+                const int x = cv[k];
+                const unsigned long long dxb = dx[k];
+                if (undirected && dxb < dub && b2d(dxb) + lw[k] == du) {
+                    if (dxb < best) { best = dxb; cnt = 1; ba = a + k; bx = x; }
+                    else if (dxb == best) ++cnt;
+                }
+                const unsigned long long nb = d2b(du + lw[k]);
+                if (nb < dxb) {
+                    // fire-and-forget: a losing min only leaves a spurious
+                    // pending bit (the vertex is re-scanned, idempotent)
+                    atomicMin(&c.dist[x], nb);
+                    atomicOr(&c.pend[x >> 5], 1u << (x & 31));
+                }
+            }
+        }
+    }
+    if (!undirected && u != s) {
+        const int b0 = g.inPtr[u], b1 = g.inPtr[u + 1];
+        for (int a = b0 + lane * UNR; a < b1; a += W * UNR) {
+            int cv[UNR];
+            double lw[UNR];
+#pragma unroll
+            for (int k = 0; k < UNR; ++k)
+                if (a + k < b1) { cv[k] = g.inCol[a + k]; lw[k] = g.inLat[a + k]; }
+#pragma unroll
+            for (int k = 0; k < UNR; ++k) {
+                if (a + k < b1) {
+                    const unsigned long long dxb = ld_relaxed(&c.dist[cv[k]]);
+                    if (dxb < dub && b2d(dxb) + lw[k] == du) {
+                        if (dxb < best) { best = dxb; cnt = 1; ba = a + k; bx = cv[k]; }
+                        else if (dxb == best) ++cnt;
+                    }
+                }
+            }
+        }
+    }
+    if (W > 1) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long ob = __shfl_xor(best, o, 64);
+            const int oc = __shfl_xor(cnt, o, 64);
+            const int oa = __shfl_xor(ba, o, 64);
+            const int ox = __shfl_xor(bx, o, 64);
+            if (ob < best) { best = ob; cnt = oc; ba = oa; bx = ox; }
+            else if (ob == best && oa >= 0) {
+                cnt += oc;
+                if (ba < 0 || oa < ba) { ba = oa; bx = ox; }
+            }
+        }
+    }
+    if (u != s && ba >= 0 && (W == 1 || lane == 0)) {
+        c.H[u] = (typename RowCtx<LAYOUT>::HopT)(c.H[bx] + 1);
+        c.R[u] = c.R[bx] * g.inRel[ba];
     }
 }
 
 // ---------------------------------------------------------------------------
 // k_sparse_rows
 // ---------------------------------------------------------------------------
-template <bool LDSDIST>
+template <int LAYOUT>
 __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
     DevGraph g, DevTable tab, DevScratch sc, const int32_t* __restrict__ rows, int32_t nRows,
-    uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg) {
+    uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg, int32_t* dbg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    using HopT = typename RowCtx<LAYOUT>::HopT;
     Ctrl* ctl = reinterpret_cast<Ctrl*>(smem);
     const int n = g.n;
     const int nw = (n + 31) >> 5;
     const int tid = threadIdx.x, NT = blockDim.x;
     const int lane = tid & 63, wave = tid >> 6, NWV = NT >> 6;
+    const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
 
     size_t off = 64;
-    unsigned long long* ldist = reinterpret_cast<unsigned long long*>(smem + off);
-    if (LDSDIST) off += (size_t)8 * n;
-    uint32_t* pend = reinterpret_cast<uint32_t*>(smem + off);
-    off += ((size_t)4 * nw + 15) & ~(size_t)15;
-    int32_t* queue = reinterpret_cast<int32_t*>(smem + off);
-    off += (size_t)4 * qcap;
-    int32_t* heavyQ = reinterpret_cast<int32_t*>(smem + off);
-
-    const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
-    unsigned long long* dist =
-        LDSDIST ? ldist : reinterpret_cast<unsigned long long*>(sc.dist + slot);
-    int32_t* H = sc.hops + slot;
-    double* R = sc.rel + slot;
-    int32_t* P = sc.pred + slot;
+    auto carve = [&](size_t bytes) {
+        unsigned char* p = smem + off;
+        off += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    RowCtx<LAYOUT> c;
+    if (LAYOUT >= 1) c.dist = reinterpret_cast<unsigned long long*>(carve((size_t)8 * n));
+    else c.dist = reinterpret_cast<unsigned long long*>(sc.dist + slot);
+    if (LAYOUT == 2) {
+        c.H = reinterpret_cast<HopT*>(carve((size_t)2 * n));
+        int32_t* rp = reinterpret_cast<int32_t*>(carve((size_t)4 * (n + 1)));
+        for (int v = tid; v <= n; v += NT) rp[v] = g.rowPtr[v];
+        c.rp = rp;
+    } else {
+        c.H = reinterpret_cast<HopT*>(sc.hops + slot);
+        c.rp = g.rowPtr;
+    }
+    uint32_t* heavyBits = reinterpret_cast<uint32_t*>(carve((size_t)4 * nw));
+    c.pend = reinterpret_cast<uint32_t*>(carve((size_t)4 * nw));
+    int32_t* queue = reinterpret_cast<int32_t*>(carve((size_t)4 * qcap));
+    int32_t* heavyQ = reinterpret_cast<int32_t*>(carve((size_t)4 * hcap));
+    c.R = sc.rel + slot;
+    c.P = sc.pred + slot;
+    for (int w = tid; w < nw; w += NT) {
+        uint32_t m = 0;
+        for (int k = 0; k < 32; ++k) {
+            const int v = (w << 5) + k;
+            if (v < n && g.rowPtr[v + 1] - g.rowPtr[v] >= heavyDeg) m |= 1u << k;
+        }
+        heavyBits[w] = m;
+    }
 
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
         const int r = rows[b];
         const int s = g.attached[r];
-        for (int v = tid; v < n; v += NT) dist[v] = INF_BITS;
-        for (int w = tid; w < nw; w += NT) pend[w] = 0u;
+        for (int v = tid; v < n; v += NT) c.dist[v] = INF_BITS;
+        for (int w = tid; w < nw; w += NT) c.pend[w] = 0u;
         if (tid == 0) {
             ctl->qtail[0] = ctl->qtail[1] = 0;
             ctl->htail[0] = ctl->htail[1] = 0;
@@ -183,42 +326,73 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         }
         __syncthreads();
         if (tid == 0) {
-            dist[s] = d2b(0.0);
-            pend[s >> 5] = 1u << (s & 31);
-            H[s] = 0;
-            R[s] = 1.0;
-            P[s] = -1;
+            c.dist[s] = d2b(0.0);
+            c.pend[s >> 5] = 1u << (s & 31);
+            c.H[s] = 0;
+            c.R[s] = 1.0;
+            c.P[s] = -1;
         }
         __syncthreads();
 
         // ---------------- delta-stepping (label-correcting) ----------------
-        int par = 0;
+        int par = 0, phases = 0;
         double bound = delta;
+        long long cScan = 0, cRelax = 0, tA = clock64(), tB;
         for (;;) {
             unsigned long long myMin = INF_BITS;
-            for (int w = tid; w < nw; w += NT) {
-                const uint32_t bits = pend[w];
-                if (!bits) continue;
-                uint32_t x = bits, taken = 0;
-                while (x) {
-                    const int bb = __ffs(x) - 1;
-                    x &= x - 1;
-                    const int v = (w << 5) + bb;
-                    const unsigned long long d = dist[v];
-                    if (b2d(d) < bound) {
-                        const int deg = g.rowPtr[v + 1] - g.rowPtr[v];
-                        if (deg >= heavyDeg) {
-                            const int pos = atomicAdd(&ctl->htail[par], 1);
-                            if (pos < hcap) { heavyQ[pos] = v; taken |= 1u << bb; }
+            for (int w0 = wave * 64; w0 < nw; w0 += NT) {
+                const int w = w0 + lane;
+                const uint32_t bits = w < nw ? c.pend[w] : 0u;
+                uint32_t tl = 0, th = 0;
+                if (bits) {
+                    const uint32_t hv = heavyBits[w];
+                    uint32_t x = bits;
+                    while (x) {
+                        const int bb = __ffs(x) - 1;
+                        x &= x - 1;
+                        const unsigned long long d = c.dist[(w << 5) + bb];
+                        if (b2d(d) < bound) {
+                            if ((hv >> bb) & 1u) th |= 1u << bb; else tl |= 1u << bb;
                         } else {
-                            const int pos = atomicAdd(&ctl->qtail[par], 1);
-                            if (pos < qcap) { queue[pos] = v; taken |= 1u << bb; }
+                            myMin = d < myMin ? d : myMin;
                         }
-                    } else {
-                        myMin = d < myMin ? d : myMin;
                     }
                 }
-                if (taken) pend[w] = bits & ~taken;
+                // wave-aggregated reservation: one LDS atomic per wave and queue
+                int nl = __popc(tl), nh = __popc(th);
+                int pl = nl, ph = nh;                       // inclusive wave scans
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int yl = __shfl_up(pl, o, 64), yh = __shfl_up(ph, o, 64);
+                    if (lane >= o) { pl += yl; ph += yh; }
+                }
+                const int totl = __shfl(pl, 63, 64), toth = __shfl(ph, 63, 64);
+                int basel = 0, baseh = 0;
+                if (lane == 0) {
+                    if (totl) basel = atomicAdd(&ctl->qtail[par], totl);
+                    if (toth) baseh = atomicAdd(&ctl->htail[par], toth);
+                }
+                basel = __shfl(basel, 0, 64) + pl - nl;
+                baseh = __shfl(baseh, 0, 64) + ph - nh;
+                if (tl | th) {
+                    uint32_t taken = 0, x = tl;
+                    int pos = basel;
+                    while (x && pos < qcap) {
+                        const int bb = __ffs(x) - 1;
+                        x &= x - 1;
+                        queue[pos++] = (w << 5) + bb;
+                        taken |= 1u << bb;
+                    }
+                    x = th;
+                    pos = baseh;
+                    while (x && pos < hcap) {
+                        const int bb = __ffs(x) - 1;
+                        x &= x - 1;
+                        heavyQ[pos++] = (w << 5) + bb;
+                        taken |= 1u << bb;
+                    }
+                    c.pend[w] = bits & ~taken;
+                }
             }
             myMin = wave_min_u64(myMin);
             if (lane == 0 && myMin != INF_BITS) atomicMin(&ctl->minNext[par], myMin);
@@ -231,6 +405,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                 ctl->htail[par ^ 1] = 0;
                 ctl->minNext[par ^ 1] = INF_BITS;
             }
+            tB = clock64(); cScan += tB - tA; tA = tB;
             if (qn == 0 && hn == 0) {
                 if (mn == INF_BITS) break;
                 const double m = b2d(mn);
@@ -240,48 +415,12 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                 __syncthreads();
                 continue;
             }
-            // light vertices: one thread per vertex
-            for (int i = tid; i < qn; i += NT) {
-                const int u = queue[i];
-                const double du = b2d(ld_relaxed(&dist[u]));
-                const int hu = H[u];
-                const double ru = R[u];
-                const int a1 = g.rowPtr[u + 1];
-                for (int a = g.rowPtr[u]; a < a1; ++a) {
-                    const int v = g.col[a];
-                    const unsigned long long nb = d2b(du + g.lat[a]);
-                    if (nb < ld_relaxed(&dist[v])) {
-                        const unsigned long long old = atomicMin(&dist[v], nb);
-                        if (nb < old) {
-                            atomicOr(&pend[v >> 5], 1u << (v & 31));
-                            H[v] = hu + 1;
-                            R[v] = ru * g.rel[a];
-                        }
-                    }
-                }
-            }
-            // heavy vertices: one wave per vertex, lanes stride the arcs
-            for (int i = wave; i < hn; i += NWV) {
-                const int u = heavyQ[i];
-                const double du = b2d(ld_relaxed(&dist[u]));
-                const int hu = H[u];
-                const double ru = R[u];
-                const int a1 = g.rowPtr[u + 1];
-                for (int a = g.rowPtr[u] + lane; a < a1; a += 64) {
-                    const int v = g.col[a];
-                    const unsigned long long nb = d2b(du + g.lat[a]);
-                    if (nb < ld_relaxed(&dist[v])) {
-                        const unsigned long long old = atomicMin(&dist[v], nb);
-                        if (nb < old) {
-                            atomicOr(&pend[v >> 5], 1u << (v & 31));
-                            H[v] = hu + 1;
-                            R[v] = ru * g.rel[a];
-                        }
-                    }
-                }
-            }
+            for (int i = tid; i < qn; i += NT) process_vertex<1, LAYOUT>(g, c, queue[i], s, 0);
+            for (int i = wave; i < hn; i += NWV) process_vertex<64, LAYOUT>(g, c, heavyQ[i], s, lane);
+            ++phases;
             par ^= 1;
             __syncthreads();
+            tB = clock64(); cRelax += tB - tA; tA = tB;
         }
 
         // ---------------- predecessor pass + tie detector -------------------
@@ -293,49 +432,67 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         int myAmb = 0, myMis = 0;
         for (int v = tid; v < n; v += NT) {
             if (v == s) continue;
-            const unsigned long long dvb = dist[v];
-            if (dvb == INF_BITS) { P[v] = -1; continue; }
+            const unsigned long long dvb = c.dist[v];
+            if (dvb == INF_BITS) { c.P[v] = -1; continue; }
             const double dv = b2d(dvb);
             unsigned long long best = INF_BITS;
-            int cnt = 0, ba = -1;
-            const int a1 = g.inPtr[v + 1];
-            for (int a = g.inPtr[v]; a < a1; ++a) {
-                const int u = g.inCol[a];
-                const unsigned long long dub = dist[u];
-                if (dub > dvb) continue;
-                if (b2d(dub) + g.inLat[a] == dv) {
-                    if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
-                    if (dub < best) { best = dub; cnt = 1; ba = a; }
-                    else if (dub == best) ++cnt;
+            int cnt = 0, ba = -1, bu = -1;
+            const int a0 = g.inPtr[v], a1 = g.inPtr[v + 1];
+            for (int a = a0; a < a1; a += UNR) {
+                int cu[UNR];
+                double lw[UNR];
+#pragma unroll
+                for (int k = 0; k < UNR; ++k)
+                    if (a + k < a1) { cu[k] = g.inCol[a + k]; lw[k] = g.inLat[a + k]; }
+#pragma unroll
+                for (int k = 0; k < UNR; ++k) {
+                    if (a + k < a1) {
+                        const unsigned long long dub = c.dist[cu[k]];
+                        if (dub <= dvb && b2d(dub) + lw[k] == dv) {
+                            if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
+                            if (dub < best) { best = dub; cnt = 1; ba = a + k; bu = cu[k]; }
+                            else if (dub == best) ++cnt;
+                        }
+                    }
                 }
             }
-            if (cnt != 1) { myAmb = 1; if (ba < 0) { P[v] = -1; continue; } }
-            P[v] = ba;
-            const int u = g.inCol[ba];
-            if (H[v] != H[u] + 1 || R[v] != R[u] * g.inRel[ba]) myMis = 1;
+            if (cnt != 1) { myAmb = 1; if (ba < 0) { c.P[v] = -1; continue; } }
+            c.P[v] = ba;
+            if ((int)c.H[v] != (int)c.H[bu] + 1 || c.R[v] != c.R[bu] * g.inRel[ba]) myMis = 1;
         }
         if (myAmb) atomicOr(&ctl->ambig, 1);
         if (myMis) atomicOr(&ctl->mismatch, 1);
         __syncthreads();
+        const long long tFinal = clock64();
+        if (dbg && tid == 0) {
+            dbg[8 * b + 0] = phases;
+            dbg[8 * b + 2] = ctl->mismatch;
+            dbg[8 * b + 3] = ctl->ambig;
+            dbg[8 * b + 4] = (int)(cScan >> 4);
+            dbg[8 * b + 5] = (int)(cRelax >> 4);
+            dbg[8 * b + 6] = (int)((tFinal - tA) >> 4);
+        }
         if (ctl->ambig) {
             if (tid == 0) rowAmbig[b] = 1;
             __syncthreads();
             continue;
         }
-        // Optimistic labels raced: fix by Jacobi sweeps over the tree until a
-        // sweep changes nothing (then every label satisfies its equation).
+        // Labels that raced or were set from a predecessor that later stopped
+        // being the chosen one: Jacobi sweeps over the tree until a sweep
+        // changes nothing (then every label satisfies its equation).
+        int jac = 0;
         if (ctl->mismatch) {
-            for (;;) {
+            for (;; ++jac) {
                 if (tid == 0) ctl->changed = 0;
                 __syncthreads();
                 int ch = 0;
                 for (int v = tid; v < n; v += NT) {
-                    const int a = P[v];
+                    const int a = c.P[v];
                     if (v == s || a < 0) continue;
                     const int u = g.inCol[a];
-                    const int eh = H[u] + 1;
-                    const double er = R[u] * g.inRel[a];
-                    if (H[v] != eh || R[v] != er) { H[v] = eh; R[v] = er; ch = 1; }
+                    const int eh = (int)c.H[u] + 1;
+                    const double er = c.R[u] * g.inRel[a];
+                    if ((int)c.H[v] != eh || c.R[v] != er) { c.H[v] = (HopT)eh; c.R[v] = er; ch = 1; }
                 }
                 if (ch) atomicOr(&ctl->changed, 1);
                 __syncthreads();
@@ -343,9 +500,15 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                 __syncthreads();
             }
         }
-        if (tid == 0) rowAmbig[b] = 0;
-        write_row(g, tab, r, s, [&](int t) { return dist[t]; }, H, R, P, 0, tid, NT);
+        if (tid == 0) {
+            rowAmbig[b] = 0;
+            if (dbg) dbg[8 * b + 1] = jac;
+        }
+        const long long tW = clock64();
+        write_row(g, tab, r, s, [&](int t) { return c.dist[t]; },
+                  [&](int t) { return (int)c.H[t]; }, c.R, c.P, 0, tid, NT);
         __syncthreads();
+        if (dbg && tid == 0) dbg[8 * b + 7] = (int)((clock64() - tW) >> 4);
     }
 }
 
@@ -490,7 +653,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g, DevTable 
         __syncthreads();
         write_row(g, tab, r, s,
                   [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
-                  H, R, P, F_EXACT, lane, EX_THREADS);
+                  [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
         __syncthreads();
     }
 }
@@ -541,25 +704,29 @@ __global__ __launch_bounds__(256) void k_direct_rows(DevGraph g, DevTable tab,
 // ---------------------------------------------------------------------------
 int sparse_max_threads() { return SP_THREADS; }
 
+template <int L>
+static void launch_sparse_layout(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                                 const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
+                                 const SparseLaunch& cfg, int32_t* dDbg, hipStream_t st, int grid) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<L>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
+    hipLaunchKernelGGL(k_sparse_rows<L>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
+                       sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap, cfg.heavyDeg,
+                       dDbg);
+}
+
 void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
-                        const SparseLaunch& cfg, void* stream) {
+                        const SparseLaunch& cfg, int32_t* dDbg, void* stream) {
     if (nRows <= 0) return;
     const int grid = nRows < cfg.grid ? nRows : cfg.grid;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (cfg.ldsDist) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-        hipLaunchKernelGGL(k_sparse_rows<true>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st,
-                           g, tab, sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap,
-                           cfg.heavyDeg);
-    } else {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-        hipLaunchKernelGGL(k_sparse_rows<false>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st,
-                           g, tab, sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap,
-                           cfg.heavyDeg);
-    }
+    if (cfg.layout == 2)
+        launch_sparse_layout<2>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+    else if (cfg.layout == 1)
+        launch_sparse_layout<1>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+    else
+        launch_sparse_layout<0>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
 }
 
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,

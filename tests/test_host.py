@@ -1,0 +1,170 @@
+"""CPU tests of the host side: GraphML reader, generators, the C-ABI library
+(loads, exports every symbol of include/shd_pathengine.h, fails loudly with no
+GPU), and the N>1 shard/gather logic on gloo."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from shdpe import generators as G
+from shdpe.graph import Topology, read_graphml, write_graphml
+
+HEADER = os.path.join(ROOT, "include", "shd_pathengine.h")
+
+
+def _declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(shd_(?:pe|topology)_\w+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    so = os.path.join(ROOT, "shadow-1_amd", "libshdpe.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "shadow-1_amd")], check=True)
+    from shdpe import engine
+    return engine.load_library()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    syms = _declared_symbols()
+    assert len(syms) >= 25
+    out = subprocess.run(["nm", "-D", "--defined-only",
+                          os.path.join(ROOT, "shadow-1_amd", "libshdpe.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (\w+)", out))
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    from shdpe import engine
+    assert sorted(engine.EXPORTS) == syms
+
+
+def test_library_is_gfx950_code_object():
+    so = os.path.join(ROOT, "shadow-1_amd", "libshdpe.so")
+    data = open(so, "rb").read()
+    assert b"gfx950" in data
+    assert b"k_sparse_rows" in data and b"k_exact_rows" in data and b"k_direct_rows" in data
+
+
+def test_engine_fails_loudly_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from shdpe.engine import Engine, EngineError, ENODEV
+    top = G.random_sparse(20, 3, seed=1)
+    with pytest.raises(EngineError) as ei:
+        Engine(top, np.arange(20))
+    assert ei.value.code == ENODEV
+
+
+def test_strerror(lib):
+    from shdpe.engine import strerror
+    assert "multigraph" in strerror(-6)
+    assert strerror(0) == "ok"
+
+
+def test_graphml_roundtrip():
+    top = G.random_sparse(30, 4, seed=3, vloss=True)
+    top.ids = ["n%d" % i for i in range(30)]
+    back = read_graphml(write_graphml(top))
+    assert back.n == top.n and back.m == top.m
+    assert np.array_equal(back.src, top.src) and np.array_equal(back.dst, top.dst)
+    assert np.array_equal(back.latency, top.latency) and np.array_equal(back.loss, top.loss)
+    assert np.array_equal(np.isnan(back.vloss), np.isnan(top.vloss))
+
+
+def test_graphml_prefers_direct_flag():
+    top = G.random_sparse(5, 2, seed=1)
+    top.prefers_direct = True
+    assert read_graphml(write_graphml(top)).prefers_direct
+
+
+def test_shipped_fixture_matches_survey():
+    top = Topology.load_npz(os.path.join(GOLDEN, "shipped_topology.npz"))
+    top.validate()
+    assert top.n == 183 and top.m == 16836
+    assert np.all(top.loss == 0.005)
+    assert np.all(top.vloss == 0.0)
+    assert top.latency.min() == 5.0
+    assert abs(top.latency.max() - 2293.85) < 1e-9
+
+
+def test_generators_are_connected_with_self_loops():
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import connected_components
+    for top in (G.rgg(3000, seed=1), G.power_law(3000, m=3, seed=4),
+                G.random_sparse(100, 3, seed=2, directed=True)):
+        top.validate()
+        loops = top.src == top.dst
+        assert np.array_equal(np.sort(top.src[loops]), np.arange(top.n))
+        A = sp.coo_matrix((np.ones(top.m), (top.src, top.dst)), shape=(top.n, top.n))
+        nc, _ = connected_components(A, directed=top.directed, connection="strong")
+        assert nc == 1
+
+
+def test_config_c2_shape():
+    top, att = G.make_config("c2")
+    assert top.n == 10_000 and att.shape[0] == 10_000
+    nl = top.src != top.dst
+    assert 40_000 < int(nl.sum()) < 60_000      # mean degree ~10
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path[:0] = [os.path.join(ROOT, "shadow-1_amd"), os.path.join(ROOT, "oracle"), ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+
+    import bench
+    import oracle as O
+    top = G.random_sparse(120, 4, seed=5)
+    att = np.arange(0, 120, 1, dtype=np.int32)
+    T = att.shape[0]
+    start, count = bench.shard(T, rank, world)
+    og = O.OracleGraph(top)
+    # the oracle stands in for the engine here (CPU test of the shard logic)
+    mine = og.rows(att[start:start + count], att)["lat"]
+    blk = (T + world - 1) // world
+    buf = torch.zeros(blk * T, dtype=torch.float64)
+    buf[: count * T] = torch.from_numpy(mine.ravel())
+    full = torch.empty(world * blk * T, dtype=torch.float64)
+    dist.all_gather_into_tensor(full, buf)
+    table = np.concatenate([full[r * blk * T: r * blk * T + bench.shard(T, r, world)[1] * T].numpy()
+                            for r in range(world)]).reshape(T, T)
+    if rank == 0:
+        ref = og.rows(att, att)["lat"]
+        q.put(bool(np.array_equal(table.view(np.int64), ref.view(np.int64))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_and_allgather_world2_gloo(oracle_mod):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok
+
+
+def test_shard_partition():
+    import bench
+    for T in (1, 7, 10_000, 65_536):
+        for world in (1, 2, 3, 8):
+            parts = [bench.shard(T, r, world) for r in range(world)]
+            assert parts[0][0] == 0
+            for (s0, c0), (s1, _) in zip(parts, parts[1:]):
+                assert s0 + c0 == s1
+            assert sum(c for _, c in parts) == T
+            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1

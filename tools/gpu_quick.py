@@ -36,12 +36,10 @@ tot += cmp(G.random_sparse(300, 6, 9, quantum=1.0), np.arange(300), tag="quantiz
 tot += cmp(G.random_sparse(300, 6, 9, quantum=1.0), np.arange(300), force=3, tag="forced-exact")
 print("TOTAL BAD", tot, flush=True)
 top, att = G.make_config("c2")
-for f in [2.0, 4.0, 8.0, 16.0]:
-    os.environ["SHDPE_DELTA_FACTOR"] = str(f)
-    eng = Engine(top, att)
-    eng.compute_positions(0, 512)
-    eng.reset_stats()
-    t0 = time.time(); eng.compute_all(); dt = time.time() - t0
-    st = eng.stats()
-    print(f"C2 factor={f} delta={st['deltaUsed']:.2f}: wall={dt:.3f}s sparse_ms={st['msSparseKernel']:.1f} exact_rows={st['rowsExact']} exact_ms={st['msExactKernel']:.1f} rows/s={10000/(st['msTotal']/1e3):.0f}", flush=True)
+os.environ["SHDPE_DEBUG"] = "1"
+for lay, thr, f in [("2", "1024", "16"), ("2", "512", "16"), ("1", "512", "16"), ("0", "256", "16"), ("0", "512", "16"), ("0", "256", "4")]:
+    os.environ["SHDPE_LAYOUT"] = lay; os.environ["SHDPE_THREADS"] = thr; os.environ["SHDPE_DELTA_FACTOR"] = f
+    eng = Engine(top, att); eng.compute_positions(0, 512); eng.reset_stats()
+    eng.compute_all(); st = eng.stats()
+    print(f"C2 layout={lay} threads={thr} f={f}: sparse_ms={st['msSparseKernel']:.1f} rows/s={10000/(st['msTotal']/1e3):.0f}", flush=True)
     eng.close()
