@@ -113,7 +113,7 @@ static void configure(ShdPe* pe) {
     const long nw = (n + 31) / 32;
     const int LDS = 160 * 1024;
     SparseLaunch c{};
-    c.threads = env_int("SHDPE_THREADS", 1024);
+    c.threads = env_int("SHDPE_THREADS", 512);
     if (c.threads > sparse_max_threads()) c.threads = sparse_max_threads();
     c.hcap = 256;
     c.heavyDeg = env_int("SHDPE_HEAVY_DEG", 64);
@@ -131,6 +131,8 @@ static void configure(ShdPe* pe) {
     }
     c.layout = layout;
     c.qcap = (int)std::min<long>((LDS - used) / 4, std::max<long>(n, 1024));
+    const int qenv = env_int("SHDPE_QCAP", layout == 0 ? 2048 : 0);
+    if (qenv > 0) c.qcap = std::min(c.qcap, qenv);
     c.qcap &= ~3;
     c.ldsBytes = used + 4 * c.qcap;
     const int maxWG = env_int("SHDPE_WG_PER_CU", 8);
@@ -276,7 +278,7 @@ static int ensure_table(ShdPe* pe) {
     pe->dRowAmbig = (uint8_t*)amb;
     if (env_int("SHDPE_DEBUG", 0)) {
         void* dbg;
-        if ((rc = dev_alloc(pe, &dbg, (size_t)pe->rowsCap * 32))) return rc;
+        if ((rc = dev_alloc(pe, &dbg, (size_t)pe->rowsCap * 64))) return rc;
         pe->dDbg = (int32_t*)dbg;
     }
     pe->tableReady = true;
@@ -328,23 +330,37 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
             for (int32_t i = 0; i < cnt; ++i)
                 if (amb[i]) exactRows.push_back(pos[c0 + i]);
             if (pe->dDbg) {
-                std::vector<int32_t> dbg((size_t)cnt * 8);
+                std::vector<int32_t> dbg((size_t)cnt * 16);
                 HIPCHK(hipMemcpy(dbg.data(), pe->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
-                double ph = 0, cy[4] = {0, 0, 0, 0};
+                double ph = 0, cy[4] = {0, 0, 0, 0}, sub[4] = {0, 0, 0, 0};
                 int phMax = 0, jMax = 0, mis = 0, am = 0; long jSum = 0;
                 for (int32_t i = 0; i < cnt; ++i) {
-                    ph += dbg[8 * i]; phMax = std::max(phMax, dbg[8 * i]);
-                    jMax = std::max(jMax, dbg[8 * i + 1]); jSum += dbg[8 * i + 1];
-                    mis += dbg[8 * i + 2] != 0; am += dbg[8 * i + 3] != 0;
-                    for (int k = 0; k < 4; ++k) cy[k] += 16.0 * dbg[8 * i + 4 + k];
+                    const int32_t* d = dbg.data() + 16 * i;
+                    ph += d[0]; phMax = std::max(phMax, d[0]);
+                    jMax = std::max(jMax, d[1]); jSum += d[1];
+                    mis += d[2] != 0; am += d[3] != 0;
+                    for (int k = 0; k < 4; ++k) cy[k] += 16.0 * d[4 + k];
+                    for (int k = 0; k < 4; ++k) sub[k] += 16.0 * d[8 + k];
+                }
+                {
+                    double a0 = 0, a1 = 0, a2 = 0, calls = 0;
+                    for (int32_t i = 0; i < cnt; ++i) {
+                        a0 += 16.0 * dbg[16 * i + 12]; a1 += 16.0 * dbg[16 * i + 13];
+                        a2 += 16.0 * dbg[16 * i + 14]; calls += dbg[16 * i + 15];
+                    }
+                    std::fprintf(stderr, "[shdpe] group call (wave0): calls/row=%.1f cyc arcs=%.0f "
+                                 "reduce=%.0f label=%.0f\n", calls / cnt, a0 / calls, a1 / calls,
+                                 a2 / calls);
                 }
                 std::fprintf(stderr,
                              "[shdpe] sparse rows=%d phases mean=%.1f max=%d | mismatch rows=%d "
                              "jacobi rounds sum=%ld max=%d | ambiguous rows=%d | delta=%.3f | "
-                             "kcycles/row scan=%.1f relax=%.1f final=%.1f write=%.1f\n",
+                             "kcycles/row scan=%.1f relax=%.1f final=%.1f write=%.1f | "
+                             "cyc/phase bits=%.0f resv=%.0f light=%.0f heavy=%.0f\n",
                              cnt, ph / cnt, phMax, mis, jSum, jMax, am, pe->cfg.delta,
                              cy[0] / cnt / 1e3, cy[1] / cnt / 1e3, cy[2] / cnt / 1e3,
-                             cy[3] / cnt / 1e3);
+                             cy[3] / cnt / 1e3, sub[0] / ph, sub[1] / ph, sub[2] / ph,
+                             sub[3] / ph);
             }
         }
         if (!exactRows.empty()) {

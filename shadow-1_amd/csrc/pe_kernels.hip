@@ -31,7 +31,7 @@
 namespace shdpe {
 
 constexpr unsigned long long INF_BITS = 0x7FF0000000000000ull;
-constexpr int SP_THREADS = 1024;
+constexpr int SP_THREADS = 512;
 constexpr int EX_THREADS = 64;
 
 __device__ __forceinline__ double b2d(unsigned long long b) {
@@ -39,6 +39,58 @@ __device__ __forceinline__ double b2d(unsigned long long b) {
 }
 __device__ __forceinline__ unsigned long long d2b(double d) {
     return (unsigned long long)__double_as_longlong(d);
+}
+
+
+// Pointers that arrive inside by-value structs lose their address space and
+// would be accessed with flat_* instructions (which also make every wait a
+// combined vmcnt+lgkmcnt wait).  Round-tripping them through address space 1
+// lets the compiler emit global_* loads/stores/atomics.
+template <class T>
+__device__ __forceinline__ T* as_global(T* p) {
+    return (T*)((__attribute__((address_space(1))) T*)p);
+}
+
+__device__ __forceinline__ DevGraph global_view(const DevGraph& g0) {
+    DevGraph g = g0;
+    g.rowPtr = as_global(g0.rowPtr);
+    g.col = as_global(g0.col);
+    g.lat = as_global(g0.lat);
+    g.rel = as_global(g0.rel);
+    g.inPtr = as_global(g0.inPtr);
+    g.inCol = as_global(g0.inCol);
+    g.inLat = as_global(g0.inLat);
+    g.inRel = as_global(g0.inRel);
+    g.outToIn = as_global(g0.outToIn);
+    g.vrel = as_global(g0.vrel);
+    g.selfLat = as_global(g0.selfLat);
+    g.selfRel = as_global(g0.selfRel);
+    g.hasSelf = as_global(g0.hasSelf);
+    g.attached = as_global(g0.attached);
+    g.isAttached = as_global(g0.isAttached);
+    return g;
+}
+
+__device__ __forceinline__ DevTable global_view(const DevTable& t0) {
+    DevTable t = t0;
+    t.lat = as_global(t0.lat);
+    t.rel = as_global(t0.rel);
+    t.hops = as_global(t0.hops);
+    t.pred = t0.pred ? as_global(t0.pred) : nullptr;
+    t.flags = as_global(t0.flags);
+    return t;
+}
+
+__device__ __forceinline__ DevScratch global_view(const DevScratch& s0) {
+    DevScratch s = s0;
+    s.dist = as_global(s0.dist);
+    s.hops = as_global(s0.hops);
+    s.rel = as_global(s0.rel);
+    s.pred = as_global(s0.pred);
+    s.heapKey = as_global(s0.heapKey);
+    s.heapIdx = as_global(s0.heapIdx);
+    s.index2 = as_global(s0.index2);
+    return s;
 }
 
 __device__ __forceinline__ unsigned long long ld_relaxed(unsigned long long* p) {
@@ -164,6 +216,8 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab
 }
 
 constexpr int UNR = 8;   // arcs loaded per batch (independent loads in flight)
+constexpr int LPV = 4;   // lanes per light frontier vertex
+constexpr int UNRG = 4;  // arcs preloaded per lane per batch
 
 // Per-row state placement.  LAYOUT 2: dist, hops (u16), rowPtr in LDS;
 // LAYOUT 1: dist in LDS; LAYOUT 0: everything in the workgroup's HBM slot.
@@ -178,41 +232,70 @@ struct RowCtx {
     uint32_t* pend;
 };
 
-// Process one frontier vertex u: (1) pull -- find the tight in-arc with the
-// minimum dist[x] under the CURRENT distances and set u's labels (hops, rel
-// product) from it; (2) push -- relax u's out-arcs with dist[u] + w
-// (ds_min_rtn_u64 on the f64 bit pattern) and mark improved vertices pending.
-// Labels are written only by the thread (or wave) processing u, so they are
-// race-free within a phase; the final pass re-verifies every label anyway.
-// W = 1: one thread per vertex; W = 64: one wave per vertex (hubs).
-template <int W, int LAYOUT>
-__device__ __forceinline__ void process_vertex(const DevGraph& g, const RowCtx<LAYOUT>& c, int u,
-                                               int s, int lane) {
-    const unsigned long long dub = ld_relaxed(&c.dist[u]);
-    const double du = b2d(dub);
-    const bool undirected = g.inCol == g.col;
+// Lane exchange inside a group: DPP quad permutes for offsets 1 and 2 (a
+// few VALU cycles), ds_bpermute for wider groups.
+template <int LPV>
+__device__ __forceinline__ int gxor(int v, int o) {
+    if (LPV <= 4) {
+        if (o == 1) return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+        return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);               // [2,3,0,1]
+    }
+    return __shfl_xor(v, o, 64);
+}
+template <int LPV>
+__device__ __forceinline__ unsigned long long gxor64(unsigned long long v, int o) {
+    const int lo = gxor<LPV>((int)(unsigned)v, o);
+    const int hi = gxor<LPV>((int)(unsigned)(v >> 32), o);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+// Process one frontier vertex u with a group of LPV lanes (each lane preloads
+// up to UNR of u's arcs): (1) pull -- find the tight in-arc with the minimum
+// dist[x] under the CURRENT distances and set u's labels (hops, rel product)
+// from it; the candidate labels H[x]+1 and R[x]*r are loaded speculatively
+// with the arcs, so no dependent round trip follows the reduction; (2) push
+// -- relax u's out-arcs with dist[u] + w (ds_min_u64 on the f64 bit pattern)
+// and mark improved vertices pending.  Labels are written only by the group
+// leader of u; the final pass re-verifies every label anyway.  All LPV lanes
+// of a group call this with the same u (u < 0: idle group, still joins the
+// lane exchanges, so the whole wave must be active).
+template <int LPV, int LAYOUT>
+__device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LAYOUT>& c, int u,
+                                              int s, int sub, long long* st = nullptr) {
+    long long p0 = st ? clock64() : 0;
     unsigned long long best = INF_BITS;
-    int cnt = 0, ba = -1, bx = -1;
-    const int a0 = c.rp[u], a1 = c.rp[u + 1];
-    for (int a = a0 + lane * UNR; a < a1; a += W * UNR) {
-        int cv[UNR];
-        double lw[UNR];
+    int cnt = 0, ba = -1, bh = 0;   // bh: chosen predecessor vertex
+    unsigned long long br = 0;      // rel of the chosen in-arc (bits)
+    const bool undirected = g.inCol == g.col;
+    if (u >= 0) {
+        const unsigned long long dub = ld_relaxed(&c.dist[u]);
+        const double du = b2d(dub);
+        const int a0 = c.rp[u], a1 = c.rp[u + 1];
+        for (int ab = a0 + sub; ab < a1; ab += LPV * UNRG) {
+            int xs[UNRG];
+            double ws[UNRG], rs[UNRG];
+            unsigned long long dx[UNRG];
 #pragma unroll
-        for (int k = 0; k < UNR; ++k)
-            if (a + k < a1) { cv[k] = g.col[a + k]; lw[k] = g.lat[a + k]; }
-        unsigned long long dx[UNR];
+            for (int k = 0; k < UNRG; ++k) {
+                const int a = ab + k * LPV;
+                if (a < a1) { xs[k] = g.col[a]; ws[k] = g.lat[a]; rs[k] = g.rel[a]; }
+                else xs[k] = -1;
+            }
 #pragma unroll
-        for (int k = 0; k < UNR; ++k) dx[k] = (a + k < a1) ? ld_relaxed(&c.dist[cv[k]]) : 0ull;
+            for (int k = 0; k < UNRG; ++k)
+                if (xs[k] >= 0) dx[k] = ld_relaxed(&c.dist[xs[k]]);
 #pragma unroll
-        for (int k = 0; k < UNR; ++k) {
-            if (a + k < a1) {
-                const int x = cv[k];
+            for (int k = 0; k < UNRG; ++k) {
+                if (xs[k] < 0) continue;
+                const int x = xs[k];
                 const unsigned long long dxb = dx[k];
-                if (undirected && dxb < dub && b2d(dxb) + lw[k] == du) {
-                    if (dxb < best) { best = dxb; cnt = 1; ba = a + k; bx = x; }
-                    else if (dxb == best) ++cnt;
+                if (undirected && dxb < dub && b2d(dxb) + ws[k] == du) {
+                    if (dxb < best) {
+                        best = dxb; cnt = 1; ba = ab + k * LPV;
+                        bh = x; br = d2b(rs[k]);
+                    } else if (dxb == best) ++cnt;
                 }
-                const unsigned long long nb = d2b(du + lw[k]);
+                const unsigned long long nb = d2b(du + ws[k]);
                 if (nb < dxb) {
                     // fire-and-forget: a losing min only leaves a spurious
                     // pending bit (the vertex is re-scanned, idempotent)
@@ -221,44 +304,42 @@ __device__ __forceinline__ void process_vertex(const DevGraph& g, const RowCtx<L
                 }
             }
         }
-    }
-    if (!undirected && u != s) {
-        const int b0 = g.inPtr[u], b1 = g.inPtr[u + 1];
-        for (int a = b0 + lane * UNR; a < b1; a += W * UNR) {
-            int cv[UNR];
-            double lw[UNR];
-#pragma unroll
-            for (int k = 0; k < UNR; ++k)
-                if (a + k < b1) { cv[k] = g.inCol[a + k]; lw[k] = g.inLat[a + k]; }
-#pragma unroll
-            for (int k = 0; k < UNR; ++k) {
-                if (a + k < b1) {
-                    const unsigned long long dxb = ld_relaxed(&c.dist[cv[k]]);
-                    if (dxb < dub && b2d(dxb) + lw[k] == du) {
-                        if (dxb < best) { best = dxb; cnt = 1; ba = a + k; bx = cv[k]; }
-                        else if (dxb == best) ++cnt;
-                    }
+        if (!undirected && u != s) {
+            const int b1 = g.inPtr[u + 1];
+            for (int a = g.inPtr[u] + sub; a < b1; a += LPV) {
+                const int x = g.inCol[a];
+                const unsigned long long dxb = ld_relaxed(&c.dist[x]);
+                if (dxb < dub && b2d(dxb) + g.inLat[a] == du) {
+                    if (dxb < best) {
+                        best = dxb; cnt = 1; ba = a;
+                        bh = x; br = d2b(g.inRel[a]);
+                    } else if (dxb == best) ++cnt;
                 }
             }
         }
     }
-    if (W > 1) {
+    long long p1 = st ? clock64() : 0;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long ob = __shfl_xor(best, o, 64);
-            const int oc = __shfl_xor(cnt, o, 64);
-            const int oa = __shfl_xor(ba, o, 64);
-            const int ox = __shfl_xor(bx, o, 64);
-            if (ob < best) { best = ob; cnt = oc; ba = oa; bx = ox; }
-            else if (ob == best && oa >= 0) {
-                cnt += oc;
-                if (ba < 0 || oa < ba) { ba = oa; bx = ox; }
-            }
+    for (int o = LPV >> 1; o > 0; o >>= 1) {
+        const unsigned long long ob = gxor64<LPV>(best, o);
+        const int oc = gxor<LPV>(cnt, o);
+        const int oa = gxor<LPV>(ba, o);
+        const int oh = gxor<LPV>(bh, o);
+        const unsigned long long orr = gxor64<LPV>(br, o);
+        if (ob < best) { best = ob; cnt = oc; ba = oa; bh = oh; br = orr; }
+        else if (ob == best && oa >= 0) {
+            cnt += oc;
+            if (ba < 0 || oa < ba) { ba = oa; bh = oh; br = orr; }
         }
     }
-    if (u != s && ba >= 0 && (W == 1 || lane == 0)) {
-        c.H[u] = (typename RowCtx<LAYOUT>::HopT)(c.H[bx] + 1);
-        c.R[u] = c.R[bx] * g.inRel[ba];
+    long long p2 = st ? clock64() : 0;
+    if (u >= 0 && u != s && ba >= 0 && sub == 0) {
+        c.H[u] = (typename RowCtx<LAYOUT>::HopT)(c.H[bh] + 1);
+        c.R[u] = c.R[bh] * b2d(br);
+    }
+    if (st) {
+        const long long p3 = clock64();
+        st[0] += p1 - p0; st[1] += p2 - p1; st[2] += p3 - p2; st[3] += 1;
     }
 }
 
@@ -267,9 +348,12 @@ __device__ __forceinline__ void process_vertex(const DevGraph& g, const RowCtx<L
 // ---------------------------------------------------------------------------
 template <int LAYOUT>
 __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
-    DevGraph g, DevTable tab, DevScratch sc, const int32_t* __restrict__ rows, int32_t nRows,
+    DevGraph g0, DevTable tab0, DevScratch sc0, const int32_t* __restrict__ rows, int32_t nRows,
     uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg, int32_t* dbg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const DevGraph g = global_view(g0);
+    const DevTable tab = global_view(tab0);
+    const DevScratch sc = global_view(sc0);
     using HopT = typename RowCtx<LAYOUT>::HopT;
     Ctrl* ctl = reinterpret_cast<Ctrl*>(smem);
     const int n = g.n;
@@ -311,6 +395,27 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         heavyBits[w] = m;
     }
 
+
+    // ---- debug micro-probe: dependent global/LDS load latency, barrier cost
+    if (false) {
+        __syncthreads();
+        long long t0 = clock64();
+        int k = 0;
+        for (int it = 0; it < 32; ++it) k = g.col[(k + it * 97) % g.rowPtr[n]] & 1023;
+        long long t1 = clock64();
+        unsigned long long kk = k;
+        for (int it = 0; it < 32; ++it) kk = c.dist[(kk + it * 7) % n] & 1023;
+        long long t2 = clock64();
+        for (int it = 0; it < 32; ++it) __syncthreads();
+        long long t3 = clock64();
+        if (tid == 0) {
+            dbg[12] = (int)((t1 - t0) / 32);
+            dbg[13] = (int)((t2 - t1) / 32);
+            dbg[14] = (int)((t3 - t2) / 32);
+            dbg[15] = (int)(k + kk);
+        }
+    }
+
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
         const int r = rows[b];
         const int s = g.attached[r];
@@ -338,6 +443,8 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         int par = 0, phases = 0;
         double bound = delta;
         long long cScan = 0, cRelax = 0, tA = clock64(), tB;
+        long long cBits = 0, cResv = 0, cLight = 0, cHeavy = 0, tX;
+        long long pst[4] = {0, 0, 0, 0};
         for (;;) {
             unsigned long long myMin = INF_BITS;
             for (int w0 = wave * 64; w0 < nw; w0 += NT) {
@@ -358,22 +465,10 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                         }
                     }
                 }
-                // wave-aggregated reservation: one LDS atomic per wave and queue
-                int nl = __popc(tl), nh = __popc(th);
-                int pl = nl, ph = nh;                       // inclusive wave scans
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int yl = __shfl_up(pl, o, 64), yh = __shfl_up(ph, o, 64);
-                    if (lane >= o) { pl += yl; ph += yh; }
-                }
-                const int totl = __shfl(pl, 63, 64), toth = __shfl(ph, 63, 64);
-                int basel = 0, baseh = 0;
-                if (lane == 0) {
-                    if (totl) basel = atomicAdd(&ctl->qtail[par], totl);
-                    if (toth) baseh = atomicAdd(&ctl->htail[par], toth);
-                }
-                basel = __shfl(basel, 0, 64) + pl - nl;
-                baseh = __shfl(baseh, 0, 64) + ph - nh;
+                tX = clock64(); cBits += tX - tA;
+                const int nl = __popc(tl), nh = __popc(th);
+                const int basel = nl ? atomicAdd(&ctl->qtail[par], nl) : 0;
+                const int baseh = nh ? atomicAdd(&ctl->htail[par], nh) : 0;
                 if (tl | th) {
                     uint32_t taken = 0, x = tl;
                     int pos = basel;
@@ -394,8 +489,8 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                     c.pend[w] = bits & ~taken;
                 }
             }
-            myMin = wave_min_u64(myMin);
-            if (lane == 0 && myMin != INF_BITS) atomicMin(&ctl->minNext[par], myMin);
+            tX = clock64(); cResv += tX - tA;
+            if (myMin != INF_BITS) atomicMin(&ctl->minNext[par], myMin);
             __syncthreads();
             const int qn = min(ctl->qtail[par], qcap);
             const int hn = min(ctl->htail[par], hcap);
@@ -415,8 +510,20 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                 __syncthreads();
                 continue;
             }
-            for (int i = tid; i < qn; i += NT) process_vertex<1, LAYOUT>(g, c, queue[i], s, 0);
-            for (int i = wave; i < hn; i += NWV) process_vertex<64, LAYOUT>(g, c, heavyQ[i], s, lane);
+            {
+                // light vertices: LPV lanes per vertex, 64/LPV vertices per wave
+                const int grp = lane / LPV, sub = lane % LPV;
+                for (int i0 = wave * (64 / LPV); i0 < qn; i0 += NWV * (64 / LPV)) {
+                    const int i = i0 + grp;
+                    process_group<LPV, LAYOUT>(g, c, i < qn ? queue[i] : -1, s, sub,
+                                               (dbg && tid == 0) ? pst : nullptr);
+                }
+                tX = clock64(); cLight += tX - tA;
+                // heavy vertices: one wave per vertex
+                for (int i = wave; i < hn; i += NWV)
+                    process_group<64, LAYOUT>(g, c, heavyQ[i], s, lane);
+                tX = clock64(); cHeavy += tX - tA;
+            }
             ++phases;
             par ^= 1;
             __syncthreads();
@@ -465,12 +572,20 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         __syncthreads();
         const long long tFinal = clock64();
         if (dbg && tid == 0) {
-            dbg[8 * b + 0] = phases;
-            dbg[8 * b + 2] = ctl->mismatch;
-            dbg[8 * b + 3] = ctl->ambig;
-            dbg[8 * b + 4] = (int)(cScan >> 4);
-            dbg[8 * b + 5] = (int)(cRelax >> 4);
-            dbg[8 * b + 6] = (int)((tFinal - tA) >> 4);
+            dbg[16 * b + 0] = phases;
+            dbg[16 * b + 2] = ctl->mismatch;
+            dbg[16 * b + 3] = ctl->ambig;
+            dbg[16 * b + 4] = (int)(cScan >> 4);
+            dbg[16 * b + 5] = (int)(cRelax >> 4);
+            dbg[16 * b + 6] = (int)((tFinal - tA) >> 4);
+            dbg[16 * b + 8] = (int)(cBits >> 4);
+            dbg[16 * b + 9] = (int)(cResv >> 4);
+            dbg[16 * b + 10] = (int)(cLight >> 4);
+            dbg[16 * b + 11] = (int)(cHeavy >> 4);
+            dbg[16 * b + 12] = (int)(pst[0] >> 4);
+            dbg[16 * b + 13] = (int)(pst[1] >> 4);
+            dbg[16 * b + 14] = (int)(pst[2] >> 4);
+            dbg[16 * b + 15] = (int)pst[3];
         }
         if (ctl->ambig) {
             if (tid == 0) rowAmbig[b] = 1;
@@ -502,13 +617,13 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         }
         if (tid == 0) {
             rowAmbig[b] = 0;
-            if (dbg) dbg[8 * b + 1] = jac;
+            if (dbg) dbg[16 * b + 1] = jac;
         }
         const long long tW = clock64();
         write_row(g, tab, r, s, [&](int t) { return c.dist[t]; },
                   [&](int t) { return (int)c.H[t]; }, c.R, c.P, 0, tid, NT);
         __syncthreads();
-        if (dbg && tid == 0) dbg[8 * b + 7] = (int)((clock64() - tW) >> 4);
+        if (dbg && tid == 0) dbg[16 * b + 7] = (int)((clock64() - tW) >> 4);
     }
 }
 
@@ -575,10 +690,14 @@ __device__ __forceinline__ void xh_modify(XHeap& h, int v, double k) {
 }
 
 template <bool LDSIDX>
-__global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g, DevTable tab, DevScratch sc,
+__global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable tab0,
+                                                           DevScratch sc0,
                                                            const int32_t* __restrict__ rows,
                                                            int32_t nRows) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const DevGraph g = global_view(g0);
+    const DevTable tab = global_view(tab0);
+    const DevScratch sc = global_view(sc0);
     const int n = g.n;
     const int lane = threadIdx.x;
     const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
@@ -662,8 +781,10 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g, DevTable 
 // k_direct_rows: complete graphs (and prefersDirectPaths pairs): row entry =
 // _topology_lookupDirectPath (topology.c:1877-1927).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_direct_rows(DevGraph g, DevTable tab,
+__global__ __launch_bounds__(256) void k_direct_rows(DevGraph g0, DevTable tab0,
                                                      const int32_t* __restrict__ rows) {
+    const DevGraph g = global_view(g0);
+    const DevTable tab = global_view(tab0);
     const int j = blockIdx.x * 256 + threadIdx.x;
     const int r = rows[blockIdx.y];
     if (j >= g.T) return;

@@ -37,7 +37,7 @@ tot += cmp(G.random_sparse(300, 6, 9, quantum=1.0), np.arange(300), force=3, tag
 print("TOTAL BAD", tot, flush=True)
 top, att = G.make_config("c2")
 os.environ["SHDPE_DEBUG"] = "1"
-for lay, thr, f in [("2", "1024", "16"), ("2", "512", "16"), ("1", "512", "16"), ("0", "256", "16"), ("0", "512", "16"), ("0", "256", "4")]:
+for lay, thr, f in [("2", "512", "16")]:
     os.environ["SHDPE_LAYOUT"] = lay; os.environ["SHDPE_THREADS"] = thr; os.environ["SHDPE_DELTA_FACTOR"] = f
     eng = Engine(top, att); eng.compute_positions(0, 512); eng.reset_stats()
     eng.compute_all(); st = eng.stats()
