@@ -17,12 +17,20 @@
 
 namespace shdpe {
 
+// One out-arc, 16 bytes: a single global_load_dwordx4 per arc.
+struct alignas(16) Arc {
+    double lat;
+    int32_t col;
+    int32_t pad;
+};
+
 struct DevGraph {
     int32_t n;
     int32_t T;                 // unique attached vertices (= targets)
     const int32_t* rowPtr;     // [n+1]
     const int32_t* col;        // [nArcs]
     const double* lat;
+    const Arc* arcs;           // [nArcs] AoS copy of (lat, col) for the relax loop
     const double* rel;
     const int32_t* inPtr;      // [n+1] (aliases rowPtr when undirected)
     const int32_t* inCol;
@@ -35,6 +43,7 @@ struct DevGraph {
     const uint8_t* hasSelf;    // [n]
     const int32_t* attached;   // [T]
     const uint8_t* isAttached; // [n]
+    const uint32_t* heavyBits; // [ceil(n/32)] vertices with degree >= heavyDeg
 };
 
 struct DevTable {
@@ -54,6 +63,7 @@ struct DevScratch {
     double* heapKey;   // exact kernel 2-way heap (igraph_2wheap_t data)
     int32_t* heapIdx;  // exact kernel 2-way heap (index)
     int32_t* index2;   // exact kernel: 0 never reached, 1 popped, >=2 heap pos+2
+    int32_t* queue;    // sparse LAYOUT 3: frontier queues, (stride + hcap) per slot
     int64_t stride;    // elements per slot (>= n)
 };
 
@@ -71,8 +81,10 @@ struct SparseLaunch {
     int32_t qcap;        // light frontier queue capacity
     int32_t hcap;        // heavy (wave-per-vertex) queue capacity
     int32_t heavyDeg;    // degree threshold for the heavy queue
-    int32_t layout;      // 2: dist+hops+rowPtr in LDS, 1: dist in LDS, 0: HBM slot
+    int32_t layout;      // 2: dist+hops+rowPtr in LDS, 1: dist in LDS, 0: HBM slot,
+                         // 3: dist+pending in LDS only (2 rows/CU), queues in HBM
     double delta;        // bucket width
+    int32_t kflags;      // kernel variant bits (tuning): 1 AoS arcs in relax, 2 AoS in pred pass
 };
 
 // kernels (pe_kernels.hip); all launched on `stream`.

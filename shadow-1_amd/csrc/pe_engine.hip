@@ -124,17 +124,22 @@ static void configure(ShdPe* pe) {
     int layout = 0, used = base;
     if (need2 + 4 * qmin <= LDS) { layout = 2; used = need2; }
     else if (need1 + 4 * qmin <= LDS) { layout = 1; used = need1; }
+    const int need3 = 64 + a16(8 * n) + a16(4 * nw);
     const int forced = env_int("SHDPE_LAYOUT", -1);
-    if (forced >= 0 && forced < layout) {
+    if (forced == 3 && need3 <= LDS) {
+        layout = 3;
+        used = need3;
+    } else if (forced >= 0 && forced < layout) {
         layout = forced;
         used = forced == 1 ? need1 : base;
     }
     c.layout = layout;
     c.qcap = (int)std::min<long>((LDS - used) / 4, std::max<long>(n, 1024));
+    if (layout == 3) c.qcap = (int)((n + 63) & ~63L);
     const int qenv = env_int("SHDPE_QCAP", layout == 0 ? 2048 : 0);
     if (qenv > 0) c.qcap = std::min(c.qcap, qenv);
     c.qcap &= ~3;
-    c.ldsBytes = used + 4 * c.qcap;
+    c.ldsBytes = layout == 3 ? used : used + 4 * c.qcap;
     const int maxWG = env_int("SHDPE_WG_PER_CU", 8);
     const int wgPerCU = std::max(1, std::min({maxWG, LDS / std::max(c.ldsBytes, 1),
                                               2048 / c.threads}));
@@ -142,6 +147,7 @@ static void configure(ShdPe* pe) {
     const double factor = env_double("SHDPE_DELTA_FACTOR", 16.0);
     c.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * factor;
     if (!(c.delta > 0)) c.delta = 1.0;
+    c.kflags = env_int("SHDPE_KFLAGS", 0);
     pe->cfg = c;
     pe->exactLdsIdx = (size_t)4 * n <= 64 * 1024;
     int exPerCU = pe->exactLdsIdx ? std::max(1, std::min(8, LDS / std::max<int>(4 * n, 1))) : 8;
@@ -206,9 +212,25 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
         shd_pe_destroy(pe);
         return rc;
     }
+    {
+        std::vector<Arc> arcs(g.col.size());
+        for (size_t a = 0; a < arcs.size(); ++a) arcs[a] = Arc{g.lat[a], g.col[a], 0};
+        Arc* da;
+        if ((rc = dev_upload(pe, &da, arcs))) { shd_pe_destroy(pe); return rc; }
+        d.arcs = da;
+    }
     d.rowPtr = rowPtr; d.col = col; d.lat = lat; d.rel = rel; d.outToIn = outToIn;
     d.vrel = vrel; d.selfLat = sl; d.selfRel = sr; d.hasSelf = hs; d.attached = att;
     d.isAttached = ia;
+    {
+        const int hd = pe->cfg.heavyDeg;
+        std::vector<uint32_t> hb((g.n + 31) / 32, 0u);
+        for (int32_t v = 0; v < g.n; ++v)
+            if (g.rowPtr[v + 1] - g.rowPtr[v] >= hd) hb[v >> 5] |= 1u << (v & 31);
+        uint32_t* dhb;
+        if ((rc = dev_upload(pe, &dhb, hb))) { shd_pe_destroy(pe); return rc; }
+        d.heavyBits = dhb;
+    }
     if (g.directed) {
         int32_t *ip, *ic;
         double *il, *ir;
@@ -269,6 +291,11 @@ static int ensure_table(ShdPe* pe) {
     pe->sc.heapIdx = (int32_t*)hi;
     pe->sc.index2 = (int32_t*)i2;
     pe->sc.stride = (int64_t)stride;
+    if (pe->cfg.layout == 3) {
+        void* q;
+        if ((rc = dev_alloc(pe, &q, (size_t)pe->cfg.grid * (stride + pe->cfg.hcap) * 4))) return rc;
+        pe->sc.queue = (int32_t*)q;
+    }
     pe->rowsCap = (int32_t)std::min<size_t>(T, 1 << 20);
     void *rows, *amb;
     if ((rc = dev_alloc(pe, &rows, (size_t)pe->rowsCap * 4)) ||

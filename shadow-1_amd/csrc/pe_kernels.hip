@@ -55,6 +55,7 @@ __device__ __forceinline__ DevGraph global_view(const DevGraph& g0) {
     DevGraph g = g0;
     g.rowPtr = as_global(g0.rowPtr);
     g.col = as_global(g0.col);
+    g.arcs = as_global(g0.arcs);
     g.lat = as_global(g0.lat);
     g.rel = as_global(g0.rel);
     g.inPtr = as_global(g0.inPtr);
@@ -68,6 +69,7 @@ __device__ __forceinline__ DevGraph global_view(const DevGraph& g0) {
     g.hasSelf = as_global(g0.hasSelf);
     g.attached = as_global(g0.attached);
     g.isAttached = as_global(g0.isAttached);
+    g.heavyBits = as_global(g0.heavyBits);
     return g;
 }
 
@@ -90,6 +92,7 @@ __device__ __forceinline__ DevScratch global_view(const DevScratch& s0) {
     s.heapKey = as_global(s0.heapKey);
     s.heapIdx = as_global(s0.heapIdx);
     s.index2 = as_global(s0.index2);
+    s.queue = as_global(s0.queue);
     return s;
 }
 
@@ -261,11 +264,11 @@ __device__ __forceinline__ unsigned long long gxor64(unsigned long long v, int o
 // lane exchanges, so the whole wave must be active).
 template <int LPV, int LAYOUT>
 __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LAYOUT>& c, int u,
-                                              int s, int sub, long long* st = nullptr) {
+                                              int s, int sub, int kflags,
+                                              long long* st = nullptr) {
     long long p0 = st ? clock64() : 0;
     unsigned long long best = INF_BITS;
-    int cnt = 0, ba = -1, bh = 0;   // bh: chosen predecessor vertex
-    unsigned long long br = 0;      // rel of the chosen in-arc (bits)
+    int cnt = 0, ba = -1, bh = 0;   // ba: chosen in-arc, bh: its tail vertex
     const bool undirected = g.inCol == g.col;
     if (u >= 0) {
         const unsigned long long dub = ld_relaxed(&c.dist[u]);
@@ -273,13 +276,15 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
         const int a0 = c.rp[u], a1 = c.rp[u + 1];
         for (int ab = a0 + sub; ab < a1; ab += LPV * UNRG) {
             int xs[UNRG];
-            double ws[UNRG], rs[UNRG];
+            double ws[UNRG];
             unsigned long long dx[UNRG];
 #pragma unroll
             for (int k = 0; k < UNRG; ++k) {
                 const int a = ab + k * LPV;
-                if (a < a1) { xs[k] = g.col[a]; ws[k] = g.lat[a]; rs[k] = g.rel[a]; }
-                else xs[k] = -1;
+                if (a < a1) {
+                    if (kflags & 1) { const Arc A = g.arcs[a]; xs[k] = A.col; ws[k] = A.lat; }
+                    else { xs[k] = g.col[a]; ws[k] = g.lat[a]; }
+                } else xs[k] = -1;
             }
 #pragma unroll
             for (int k = 0; k < UNRG; ++k)
@@ -292,7 +297,7 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
                 if (undirected && dxb < dub && b2d(dxb) + ws[k] == du) {
                     if (dxb < best) {
                         best = dxb; cnt = 1; ba = ab + k * LPV;
-                        bh = x; br = d2b(rs[k]);
+                        bh = x;
                     } else if (dxb == best) ++cnt;
                 }
                 const unsigned long long nb = d2b(du + ws[k]);
@@ -312,7 +317,7 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
                 if (dxb < dub && b2d(dxb) + g.inLat[a] == du) {
                     if (dxb < best) {
                         best = dxb; cnt = 1; ba = a;
-                        bh = x; br = d2b(g.inRel[a]);
+                        bh = x;
                     } else if (dxb == best) ++cnt;
                 }
             }
@@ -325,17 +330,16 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
         const int oc = gxor<LPV>(cnt, o);
         const int oa = gxor<LPV>(ba, o);
         const int oh = gxor<LPV>(bh, o);
-        const unsigned long long orr = gxor64<LPV>(br, o);
-        if (ob < best) { best = ob; cnt = oc; ba = oa; bh = oh; br = orr; }
+        if (ob < best) { best = ob; cnt = oc; ba = oa; bh = oh; }
         else if (ob == best && oa >= 0) {
             cnt += oc;
-            if (ba < 0 || oa < ba) { ba = oa; bh = oh; br = orr; }
+            if (ba < 0 || oa < ba) { ba = oa; bh = oh; }
         }
     }
     long long p2 = st ? clock64() : 0;
     if (u >= 0 && u != s && ba >= 0 && sub == 0) {
         c.H[u] = (typename RowCtx<LAYOUT>::HopT)(c.H[bh] + 1);
-        c.R[u] = c.R[bh] * b2d(br);
+        c.R[u] = c.R[bh] * g.inRel[ba];
     }
     if (st) {
         const long long p3 = clock64();
@@ -349,7 +353,8 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
 template <int LAYOUT>
 __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
     DevGraph g0, DevTable tab0, DevScratch sc0, const int32_t* __restrict__ rows, int32_t nRows,
-    uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg, int32_t* dbg) {
+    uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg, int32_t* dbg,
+    int32_t kflags) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
@@ -369,6 +374,8 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         return p;
     };
     RowCtx<LAYOUT> c;
+    // LAYOUT 3: only dist + pending bits in LDS (2 rows per CU at n = 10k);
+    // queues, hops and rowPtr live in the workgroup's HBM slot / the graph.
     if (LAYOUT >= 1) c.dist = reinterpret_cast<unsigned long long*>(carve((size_t)8 * n));
     else c.dist = reinterpret_cast<unsigned long long*>(sc.dist + slot);
     if (LAYOUT == 2) {
@@ -380,21 +387,26 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         c.H = reinterpret_cast<HopT*>(sc.hops + slot);
         c.rp = g.rowPtr;
     }
-    uint32_t* heavyBits = reinterpret_cast<uint32_t*>(carve((size_t)4 * nw));
+    const uint32_t* heavyBits;
+    if (LAYOUT == 3) {
+        heavyBits = g.heavyBits;
+    } else {
+        uint32_t* hb = reinterpret_cast<uint32_t*>(carve((size_t)4 * nw));
+        for (int w = tid; w < nw; w += NT) hb[w] = g.heavyBits[w];
+        heavyBits = hb;
+    }
     c.pend = reinterpret_cast<uint32_t*>(carve((size_t)4 * nw));
-    int32_t* queue = reinterpret_cast<int32_t*>(carve((size_t)4 * qcap));
-    int32_t* heavyQ = reinterpret_cast<int32_t*>(carve((size_t)4 * hcap));
+    int32_t* queue;
+    int32_t* heavyQ;
+    if (LAYOUT == 3) {
+        queue = sc.queue + (size_t)blockIdx.x * (size_t)(sc.stride + hcap);
+        heavyQ = queue + sc.stride;
+    } else {
+        queue = reinterpret_cast<int32_t*>(carve((size_t)4 * qcap));
+        heavyQ = reinterpret_cast<int32_t*>(carve((size_t)4 * hcap));
+    }
     c.R = sc.rel + slot;
     c.P = sc.pred + slot;
-    for (int w = tid; w < nw; w += NT) {
-        uint32_t m = 0;
-        for (int k = 0; k < 32; ++k) {
-            const int v = (w << 5) + k;
-            if (v < n && g.rowPtr[v + 1] - g.rowPtr[v] >= heavyDeg) m |= 1u << k;
-        }
-        heavyBits[w] = m;
-    }
-
 
     // ---- debug micro-probe: dependent global/LDS load latency, barrier cost
     if (false) {
@@ -455,13 +467,25 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                     const uint32_t hv = heavyBits[w];
                     uint32_t x = bits;
                     while (x) {
-                        const int bb = __ffs(x) - 1;
-                        x &= x - 1;
-                        const unsigned long long d = c.dist[(w << 5) + bb];
-                        if (b2d(d) < bound) {
-                            if ((hv >> bb) & 1u) th |= 1u << bb; else tl |= 1u << bb;
-                        } else {
-                            myMin = d < myMin ? d : myMin;
+                        // 4 pending bits at a time: independent LDS reads in flight
+                        int pb[4];
+                        unsigned long long d[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            pb[k] = x ? __ffs(x) - 1 : -1;
+                            x &= x - 1;
+                        }
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            d[k] = pb[k] >= 0 ? c.dist[(w << 5) + pb[k]] : INF_BITS;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            if (pb[k] < 0) continue;
+                            if (b2d(d[k]) < bound) {
+                                if ((hv >> pb[k]) & 1u) th |= 1u << pb[k]; else tl |= 1u << pb[k];
+                            } else {
+                                myMin = d[k] < myMin ? d[k] : myMin;
+                            }
                         }
                     }
                 }
@@ -515,13 +539,13 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                 const int grp = lane / LPV, sub = lane % LPV;
                 for (int i0 = wave * (64 / LPV); i0 < qn; i0 += NWV * (64 / LPV)) {
                     const int i = i0 + grp;
-                    process_group<LPV, LAYOUT>(g, c, i < qn ? queue[i] : -1, s, sub,
+                    process_group<LPV, LAYOUT>(g, c, i < qn ? queue[i] : -1, s, sub, kflags,
                                                (dbg && tid == 0) ? pst : nullptr);
                 }
                 tX = clock64(); cLight += tX - tA;
                 // heavy vertices: one wave per vertex
                 for (int i = wave; i < hn; i += NWV)
-                    process_group<64, LAYOUT>(g, c, heavyQ[i], s, lane);
+                    process_group<64, LAYOUT>(g, c, heavyQ[i], s, lane, kflags);
                 tX = clock64(); cHeavy += tX - tA;
             }
             ++phases;
@@ -544,13 +568,19 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
             const double dv = b2d(dvb);
             unsigned long long best = INF_BITS;
             int cnt = 0, ba = -1, bu = -1;
-            const int a0 = g.inPtr[v], a1 = g.inPtr[v + 1];
+            const bool undirected = g.inCol == g.col;
+            const int a0 = undirected ? c.rp[v] : g.inPtr[v];
+            const int a1 = undirected ? c.rp[v + 1] : g.inPtr[v + 1];
             for (int a = a0; a < a1; a += UNR) {
                 int cu[UNR];
                 double lw[UNR];
 #pragma unroll
-                for (int k = 0; k < UNR; ++k)
-                    if (a + k < a1) { cu[k] = g.inCol[a + k]; lw[k] = g.inLat[a + k]; }
+                for (int k = 0; k < UNR; ++k) {
+                    if (a + k < a1) {
+                        if (undirected && (kflags & 2)) { const Arc A = g.arcs[a + k]; cu[k] = A.col; lw[k] = A.lat; }
+                        else { cu[k] = g.inCol[a + k]; lw[k] = g.inLat[a + k]; }
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < UNR; ++k) {
                     if (a + k < a1) {
@@ -833,7 +863,7 @@ static void launch_sparse_layout(const DevGraph& g, const DevTable& tab, const D
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
     hipLaunchKernelGGL(k_sparse_rows<L>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
                        sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap, cfg.heavyDeg,
-                       dDbg);
+                       dDbg, cfg.kflags);
 }
 
 void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
@@ -842,7 +872,9 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
     if (nRows <= 0) return;
     const int grid = nRows < cfg.grid ? nRows : cfg.grid;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (cfg.layout == 2)
+    if (cfg.layout == 3)
+        launch_sparse_layout<3>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+    else if (cfg.layout == 2)
         launch_sparse_layout<2>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
     else if (cfg.layout == 1)
         launch_sparse_layout<1>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);

@@ -36,10 +36,12 @@ tot += cmp(G.random_sparse(300, 6, 9, quantum=1.0), np.arange(300), tag="quantiz
 tot += cmp(G.random_sparse(300, 6, 9, quantum=1.0), np.arange(300), force=3, tag="forced-exact")
 print("TOTAL BAD", tot, flush=True)
 top, att = G.make_config("c2")
-os.environ["SHDPE_DEBUG"] = "1"
-for lay, thr, f in [("2", "512", "16")]:
-    os.environ["SHDPE_LAYOUT"] = lay; os.environ["SHDPE_THREADS"] = thr; os.environ["SHDPE_DELTA_FACTOR"] = f
+os.environ["SHDPE_DEBUG"] = os.environ.get("QDEBUG", "1")
+for kf in os.environ.get("QKFLAGS", "0").split(","):
+  os.environ["SHDPE_KFLAGS"] = kf
+  for lay in os.environ.get("QLAYOUTS", "2,3").split(","):
+    os.environ["SHDPE_LAYOUT"] = lay
     eng = Engine(top, att); eng.compute_positions(0, 512); eng.reset_stats()
     eng.compute_all(); st = eng.stats()
-    print(f"C2 layout={lay} threads={thr} f={f}: sparse_ms={st['msSparseKernel']:.1f} rows/s={10000/(st['msTotal']/1e3):.0f}", flush=True)
+    print(f"C2 kflags={kf} layout={lay}: sparse_ms={st['msSparseKernel']:.2f} rows/s={10000/(st['msTotal']/1e3):.0f}", flush=True)
     eng.close()
