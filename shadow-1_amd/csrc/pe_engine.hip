@@ -124,12 +124,22 @@ static void configure(ShdPe* pe) {
     int layout = 0, used = base;
     if (need2 + 4 * qmin <= LDS) { layout = 2; used = need2; }
     else if (need1 + 4 * qmin <= LDS) { layout = 1; used = need1; }
+    // LAYOUT 3 keeps only dist + pending bits in LDS: ~1.4x slower per row
+    // than LAYOUT 2 (measured, C2) but fits more rows per CU; take it when it
+    // at least doubles the resident rows.
     const int need3 = 64 + a16(8 * n) + a16(4 * nw);
+    const int maxWgByThreads = 2048 / std::max(c.threads, 64);
+    const int wg2 = layout == 2 ? std::min(maxWgByThreads, LDS / (need2 + 4 * qmin)) : 0;
+    const int wg3 = std::min(maxWgByThreads, LDS / need3);
+    if (need3 <= LDS && wg3 >= 2 * std::max(wg2, 1)) { layout = 3; used = need3; }
     const int forced = env_int("SHDPE_LAYOUT", -1);
     if (forced == 3 && need3 <= LDS) {
         layout = 3;
         used = need3;
-    } else if (forced >= 0 && forced < layout) {
+    } else if (forced == 2 && need2 + 4 * qmin <= LDS) {
+        layout = 2;
+        used = need2;
+    } else if (forced >= 0 && forced < 2) {
         layout = forced;
         used = forced == 1 ? need1 : base;
     }
