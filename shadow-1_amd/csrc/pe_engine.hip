@@ -118,38 +118,36 @@ static void configure(ShdPe* pe) {
     c.hcap = 256;
     c.heavyDeg = env_int("SHDPE_HEAVY_DEG", 64);
     const int qmin = 2048;
-    const int base = 64 + 2 * a16(4 * nw) + a16(4 * c.hcap);
-    const int need2 = base + a16(8 * n) + a16(2 * n) + a16(4 * (n + 1));
-    const int need1 = base + a16(8 * n);
-    int layout = 0, used = base;
-    if (need2 + 4 * qmin <= LDS) { layout = 2; used = need2; }
-    else if (need1 + 4 * qmin <= LDS) { layout = 1; used = need1; }
+    // LDS bytes per layout (queues are ping-pong pairs; LAYOUT 0/3 keep them in HBM)
+    const int pend = a16(4 * nw), hbits = a16(4 * nw);
+    const int hq2 = 2 * a16(4 * c.hcap);
+    const int need2 = 64 + pend + hbits + hq2 + a16(8 * n) + a16(2 * n) + a16(4 * (n + 1));
+    const int need1 = 64 + pend + hbits + hq2 + a16(8 * n);
+    const int need3 = 64 + pend + a16(8 * n);
+    const int need0 = 64 + pend + hbits;
+    int layout = 0, used = need0;
+    if (need2 + 8 * qmin <= LDS) { layout = 2; used = need2; }
+    else if (need1 + 8 * qmin <= LDS) { layout = 1; used = need1; }
     // LAYOUT 3 keeps only dist + pending bits in LDS: ~1.4x slower per row
     // than LAYOUT 2 (measured, C2) but fits more rows per CU; take it when it
     // at least doubles the resident rows.
-    const int need3 = 64 + a16(8 * n) + a16(4 * nw);
     const int maxWgByThreads = 2048 / std::max(c.threads, 64);
-    const int wg2 = layout == 2 ? std::min(maxWgByThreads, LDS / (need2 + 4 * qmin)) : 0;
+    const int wg2 = layout == 2 ? std::min(maxWgByThreads, LDS / (need2 + 8 * qmin)) : 0;
     const int wg3 = std::min(maxWgByThreads, LDS / need3);
     if (need3 <= LDS && wg3 >= 2 * std::max(wg2, 1)) { layout = 3; used = need3; }
     const int forced = env_int("SHDPE_LAYOUT", -1);
-    if (forced == 3 && need3 <= LDS) {
-        layout = 3;
-        used = need3;
-    } else if (forced == 2 && need2 + 4 * qmin <= LDS) {
-        layout = 2;
-        used = need2;
-    } else if (forced >= 0 && forced < 2) {
-        layout = forced;
-        used = forced == 1 ? need1 : base;
-    }
+    if (forced == 3 && need3 <= LDS) { layout = 3; used = need3; }
+    else if (forced == 2 && need2 + 8 * qmin <= LDS) { layout = 2; used = need2; }
+    else if (forced == 1 && need1 + 8 * qmin <= LDS) { layout = 1; used = need1; }
+    else if (forced == 0) { layout = 0; used = need0; }
     c.layout = layout;
-    c.qcap = (int)std::min<long>((LDS - used) / 4, std::max<long>(n, 1024));
-    if (layout == 3) c.qcap = (int)((n + 63) & ~63L);
-    const int qenv = env_int("SHDPE_QCAP", layout == 0 ? 2048 : 0);
-    if (qenv > 0) c.qcap = std::min(c.qcap, qenv);
-    c.qcap &= ~3;
-    c.ldsBytes = layout == 3 ? used : used + 4 * c.qcap;
+    if (layout == 1 || layout == 2) {
+        c.qcap = (int)std::min<long>((LDS - used) / 8, std::max<long>(n, 1024)) & ~3;
+        c.ldsBytes = used + 2 * a16(4 * c.qcap);
+    } else {
+        c.qcap = (int)((n + 63) & ~63L);
+        c.ldsBytes = used;
+    }
     const int maxWG = env_int("SHDPE_WG_PER_CU", 8);
     const int wgPerCU = std::max(1, std::min({maxWG, LDS / std::max(c.ldsBytes, 1),
                                               2048 / c.threads}));
@@ -160,7 +158,7 @@ static void configure(ShdPe* pe) {
     c.kflags = env_int("SHDPE_KFLAGS", 0);
     pe->cfg = c;
     pe->exactLdsIdx = (size_t)4 * n <= 64 * 1024;
-    int exPerCU = pe->exactLdsIdx ? std::max(1, std::min(8, LDS / std::max<int>(4 * n, 1))) : 8;
+    int exPerCU = pe->exactLdsIdx ? (int)std::max<long>(1, std::min<long>(8, LDS / std::max<long>(4 * n, 1))) : 8;
     pe->exactGrid = pe->numCUs * exPerCU;
     pe->stats.deltaUsed = c.delta;
 }
@@ -301,9 +299,10 @@ static int ensure_table(ShdPe* pe) {
     pe->sc.heapIdx = (int32_t*)hi;
     pe->sc.index2 = (int32_t*)i2;
     pe->sc.stride = (int64_t)stride;
-    if (pe->cfg.layout == 3) {
+    if (pe->cfg.layout == 3 || pe->cfg.layout == 0) {
         void* q;
-        if ((rc = dev_alloc(pe, &q, (size_t)pe->cfg.grid * (stride + pe->cfg.hcap) * 4))) return rc;
+        const size_t per = 2 * ((size_t)pe->cfg.qcap + pe->cfg.hcap);
+        if ((rc = dev_alloc(pe, &q, (size_t)pe->cfg.grid * per * 4))) return rc;
         pe->sc.queue = (int32_t*)q;
     }
     pe->rowsCap = (int32_t)std::min<size_t>(T, 1 << 20);

@@ -233,6 +233,14 @@ struct RowCtx {
     double* R;
     int32_t* P;
     uint32_t* pend;
+    const uint32_t* heavyBits;
+    // "next" frontier queues (filled on a pending-bit 0 -> 1 transition)
+    int32_t* nq;
+    int32_t* nhq;
+    int* ntail;
+    int* nhtail;
+    int qcap, hcap;
+    double bound;
 };
 
 // Lane exchange inside a group: DPP quad permutes for offsets 1 and 2 (a
@@ -262,7 +270,7 @@ __device__ __forceinline__ unsigned long long gxor64(unsigned long long v, int o
 // leader of u; the final pass re-verifies every label anyway.  All LPV lanes
 // of a group call this with the same u (u < 0: idle group, still joins the
 // lane exchanges, so the whole wave must be active).
-template <int LPV, int LAYOUT>
+template <int LPV, int LAYOUT, bool QUEUED>
 __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LAYOUT>& c, int u,
                                               int s, int sub, int kflags,
                                               long long* st = nullptr) {
@@ -271,6 +279,9 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
     int cnt = 0, ba = -1, bh = 0;   // ba: chosen in-arc, bh: its tail vertex
     const bool undirected = g.inCol == g.col;
     if (u >= 0) {
+        // u leaves the pending set before its dist is read: an improvement
+        // racing with this processing re-sets the bit and re-queues u.
+        if (QUEUED && sub == 0) atomicAnd(&c.pend[u >> 5], ~(1u << (u & 31)));
         const unsigned long long dub = ld_relaxed(&c.dist[u]);
         const double du = b2d(dub);
         const int a0 = c.rp[u], a1 = c.rp[u + 1];
@@ -300,12 +311,29 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
                         bh = x;
                     } else if (dxb == best) ++cnt;
                 }
-                const unsigned long long nb = d2b(du + ws[k]);
+                const double nd = du + ws[k];
+                const unsigned long long nb = d2b(nd);
                 if (nb < dxb) {
-                    // fire-and-forget: a losing min only leaves a spurious
-                    // pending bit (the vertex is re-scanned, idempotent)
+                    // a losing min only leaves a spurious pending vertex
+                    // (processed once more, idempotent)
                     atomicMin(&c.dist[x], nb);
-                    atomicOr(&c.pend[x >> 5], 1u << (x & 31));
+                    const uint32_t bit = 1u << (x & 31);
+                    if (!QUEUED) {
+                        atomicOr(&c.pend[x >> 5], bit);      // fire-and-forget
+                        continue;
+                    }
+                    const uint32_t old = atomicOr(&c.pend[x >> 5], bit);
+                    if (!(old & bit) && nd < c.bound) {
+                        // newly pending inside the bucket -> next frontier;
+                        // on overflow it stays pending for the bucket scan
+                        if ((c.heavyBits[x >> 5] >> (x & 31)) & 1u) {
+                            const int pos = atomicAdd(c.nhtail, 1);
+                            if (pos < c.hcap) c.nhq[pos] = x;
+                        } else {
+                            const int pos = atomicAdd(c.ntail, 1);
+                            if (pos < c.qcap) c.nq[pos] = x;
+                        }
+                    }
                 }
             }
         }
@@ -360,6 +388,10 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
     using HopT = typename RowCtx<LAYOUT>::HopT;
+    // Frontier: queue-driven (filled by relaxations) when the row lives in
+    // HBM (large n: a bitmask scan would read dist from HBM every phase);
+    // bitmask scan per phase when dist is in LDS (cheaper relax step).
+    constexpr bool QMODE = LAYOUT == 0;
     Ctrl* ctl = reinterpret_cast<Ctrl*>(smem);
     const int n = g.n;
     const int nw = (n + 31) >> 5;
@@ -395,16 +427,25 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         for (int w = tid; w < nw; w += NT) hb[w] = g.heavyBits[w];
         heavyBits = hb;
     }
+    c.heavyBits = heavyBits;
     c.pend = reinterpret_cast<uint32_t*>(carve((size_t)4 * nw));
-    int32_t* queue;
-    int32_t* heavyQ;
-    if (LAYOUT == 3) {
-        queue = sc.queue + (size_t)blockIdx.x * (size_t)(sc.stride + hcap);
-        heavyQ = queue + sc.stride;
+    // ping-pong frontier queues Q[0], Q[1] (light) and HQ[0], HQ[1] (heavy)
+    int32_t* Q[2];
+    int32_t* HQ[2];
+    if (LAYOUT == 3 || LAYOUT == 0) {
+        int32_t* base = sc.queue + (size_t)blockIdx.x * (size_t)(2 * (qcap + hcap));
+        Q[0] = base;
+        Q[1] = base + qcap;
+        HQ[0] = base + 2 * qcap;
+        HQ[1] = base + 2 * qcap + hcap;
     } else {
-        queue = reinterpret_cast<int32_t*>(carve((size_t)4 * qcap));
-        heavyQ = reinterpret_cast<int32_t*>(carve((size_t)4 * hcap));
+        Q[0] = reinterpret_cast<int32_t*>(carve((size_t)4 * qcap));
+        Q[1] = reinterpret_cast<int32_t*>(carve((size_t)4 * qcap));
+        HQ[0] = reinterpret_cast<int32_t*>(carve((size_t)4 * hcap));
+        HQ[1] = reinterpret_cast<int32_t*>(carve((size_t)4 * hcap));
     }
+    c.qcap = qcap;
+    c.hcap = hcap;
     c.R = sc.rel + slot;
     c.P = sc.pred + slot;
 
@@ -445,18 +486,135 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         if (tid == 0) {
             c.dist[s] = d2b(0.0);
             c.pend[s >> 5] = 1u << (s & 31);
+            if (QMODE) {
+                if ((heavyBits[s >> 5] >> (s & 31)) & 1u) { HQ[0][0] = s; ctl->htail[0] = 1; }
+                else { Q[0][0] = s; ctl->qtail[0] = 1; }
+            }
             c.H[s] = 0;
             c.R[s] = 1.0;
             c.P[s] = -1;
         }
         __syncthreads();
 
-        // ---------------- delta-stepping (label-correcting) ----------------
-        int par = 0, phases = 0;
-        double bound = delta;
+        int phases = 0;
         long long cScan = 0, cRelax = 0, tA = clock64(), tB;
         long long cBits = 0, cResv = 0, cLight = 0, cHeavy = 0, tX;
         long long pst[4] = {0, 0, 0, 0};
+        if (QMODE) {
+        // ---------------- delta-stepping (label-correcting) ----------------
+        // Frontier = queue filled by the previous phase's relaxations; the
+        // pending bitmask is scanned only when a bucket's queue runs dry.
+        int par = 0;
+        double bound = delta;
+        for (;;) {
+            int qn = min(ctl->qtail[par], qcap);
+            int hn = min(ctl->htail[par], hcap);
+            if (qn == 0 && hn == 0) {
+                // bucket drained: collect pending vertices below the bound
+                __syncthreads();
+                if (tid == 0) {
+                    ctl->qtail[par] = 0;
+                    ctl->htail[par] = 0;
+                    ctl->minNext[0] = INF_BITS;
+                }
+                __syncthreads();
+                unsigned long long myMin = INF_BITS;
+                for (int w0 = wave * 64; w0 < nw; w0 += NT) {
+                    const int w = w0 + lane;
+                    const uint32_t bits = w < nw ? c.pend[w] : 0u;
+                    uint32_t tl = 0, th = 0;
+                    if (bits) {
+                        const uint32_t hv = heavyBits[w];
+                        uint32_t x = bits;
+                        while (x) {
+                            int pb[4];
+                            unsigned long long d[4];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                pb[k] = x ? __ffs(x) - 1 : -1;
+                                x &= x - 1;
+                            }
+#pragma unroll
+                            for (int k = 0; k < 4; ++k)
+                                d[k] = pb[k] >= 0 ? c.dist[(w << 5) + pb[k]] : INF_BITS;
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                if (pb[k] < 0) continue;
+                                if (b2d(d[k]) < bound) {
+                                    if ((hv >> pb[k]) & 1u) th |= 1u << pb[k];
+                                    else tl |= 1u << pb[k];
+                                } else {
+                                    myMin = d[k] < myMin ? d[k] : myMin;
+                                }
+                            }
+                        }
+                    }
+                    const int nl = __popc(tl), nh = __popc(th);
+                    int pl = nl ? atomicAdd(&ctl->qtail[par], nl) : 0;
+                    int ph = nh ? atomicAdd(&ctl->htail[par], nh) : 0;
+                    while (tl) {
+                        const int bb = __ffs(tl) - 1;
+                        tl &= tl - 1;
+                        if (pl < qcap) Q[par][pl] = (w << 5) + bb;
+                        ++pl;
+                    }
+                    while (th) {
+                        const int bb = __ffs(th) - 1;
+                        th &= th - 1;
+                        if (ph < hcap) HQ[par][ph] = (w << 5) + bb;
+                        ++ph;
+                    }
+                }
+                if (myMin != INF_BITS) atomicMin(&ctl->minNext[0], myMin);
+                __syncthreads();
+                qn = min(ctl->qtail[par], qcap);
+                hn = min(ctl->htail[par], hcap);
+                const unsigned long long mn = ctl->minNext[0];
+                tB = clock64(); cScan += tB - tA; tA = tB;
+                if (qn == 0 && hn == 0) {
+                    if (mn == INF_BITS) break;
+                    const double m = b2d(mn);
+                    bound = (floor(m / delta) + 1.0) * delta;
+                    if (!(m < bound)) bound = m + delta;
+                    continue;
+                }
+            }
+            c.bound = bound;
+            c.nq = Q[par ^ 1];
+            c.nhq = HQ[par ^ 1];
+            c.ntail = &ctl->qtail[par ^ 1];
+            c.nhtail = &ctl->htail[par ^ 1];
+            {
+                // light vertices: LPV lanes per vertex, 64/LPV vertices per wave
+                const int grp = lane / LPV, sub = lane % LPV;
+                int32_t* cq = Q[par];
+                for (int i0 = wave * (64 / LPV); i0 < qn; i0 += NWV * (64 / LPV)) {
+                    const int i = i0 + grp;
+                    process_group<LPV, LAYOUT, true>(g, c, i < qn ? cq[i] : -1, s, sub, kflags,
+                                               (dbg && tid == 0) ? pst : nullptr);
+                }
+                tX = clock64(); cLight += tX - tA;
+                // heavy vertices: one wave per vertex
+                int32_t* chq = HQ[par];
+                for (int i = wave; i < hn; i += NWV)
+                    process_group<64, LAYOUT, true>(g, c, chq[i], s, lane, kflags);
+                tX = clock64(); cHeavy += tX - tA;
+            }
+            ++phases;
+            __syncthreads();
+            if (tid == 0) {
+                ctl->qtail[par] = 0;
+                ctl->htail[par] = 0;
+            }
+            par ^= 1;
+            __syncthreads();
+            tB = clock64(); cRelax += tB - tA; tA = tB;
+        }
+
+        } else {
+        // ---------------- delta-stepping (label-correcting) ----------------
+        int par = 0;
+        double bound = delta;
         for (;;) {
             unsigned long long myMin = INF_BITS;
             for (int w0 = wave * 64; w0 < nw; w0 += NT) {
@@ -499,7 +657,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                     while (x && pos < qcap) {
                         const int bb = __ffs(x) - 1;
                         x &= x - 1;
-                        queue[pos++] = (w << 5) + bb;
+                        Q[0][pos++] = (w << 5) + bb;
                         taken |= 1u << bb;
                     }
                     x = th;
@@ -507,7 +665,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                     while (x && pos < hcap) {
                         const int bb = __ffs(x) - 1;
                         x &= x - 1;
-                        heavyQ[pos++] = (w << 5) + bb;
+                        HQ[0][pos++] = (w << 5) + bb;
                         taken |= 1u << bb;
                     }
                     c.pend[w] = bits & ~taken;
@@ -539,13 +697,13 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                 const int grp = lane / LPV, sub = lane % LPV;
                 for (int i0 = wave * (64 / LPV); i0 < qn; i0 += NWV * (64 / LPV)) {
                     const int i = i0 + grp;
-                    process_group<LPV, LAYOUT>(g, c, i < qn ? queue[i] : -1, s, sub, kflags,
+                    process_group<LPV, LAYOUT, false>(g, c, i < qn ? Q[0][i] : -1, s, sub, kflags,
                                                (dbg && tid == 0) ? pst : nullptr);
                 }
                 tX = clock64(); cLight += tX - tA;
                 // heavy vertices: one wave per vertex
                 for (int i = wave; i < hn; i += NWV)
-                    process_group<64, LAYOUT>(g, c, heavyQ[i], s, lane, kflags);
+                    process_group<64, LAYOUT, false>(g, c, HQ[0][i], s, lane, kflags);
                 tX = clock64(); cHeavy += tX - tA;
             }
             ++phases;
@@ -554,6 +712,7 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
             tB = clock64(); cRelax += tB - tA; tA = tB;
         }
 
+        }
         // ---------------- predecessor pass + tie detector -------------------
         // igraph sets parent[v] on the first strict improvement to the final
         // distance, i.e. from the first POPPED tight predecessor; pops are in
