@@ -77,7 +77,8 @@ typedef struct ShdPeOptions {
     double delta;            /* delta-stepping bucket width (ms); 0 = auto        */
     int32_t storePred;       /* keep a predecessor-vertex column in the table      */
     int32_t forceMode;       /* 0 auto, 1 sparse delta-stepping, 2 direct gather,
-                                3 exact igraph-heap kernel for every row (tests)  */
+                                3 exact igraph-heap kernel for every row (tests),
+                                4 dense blocked min-plus                          */
 } ShdPeOptions;
 
 typedef struct ShdPe ShdPe;
@@ -92,12 +93,15 @@ typedef struct ShdPeStats {
     double msDirectKernel;     /* device time of the direct-gather kernel         */
     double msTotal;            /* device time of whole compute calls              */
     int64_t launchesSparse, launchesExact, launchesDirect;
-    int32_t mode;              /* 1 sparse, 2 direct (complete graph)              */
+    int32_t mode;              /* 1 sparse, 2 direct (complete graph), 3 dense     */
     int32_t isComplete;        /* _topology_isComplete() of the graph              */
     int32_t nVertices;
     int64_t nArcs;             /* non-loop arcs (undirected edge = 2 arcs)         */
     int32_t nAttached;
     double deltaUsed;
+    double msDenseKernel;      /* device time of the dense min-plus path           */
+    int64_t launchesDense;
+    int64_t denseSweeps;       /* min-plus sweeps (incl. the confirming one)       */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */

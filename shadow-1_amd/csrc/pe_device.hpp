@@ -97,5 +97,12 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
 void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
                         int32_t nRows, void* stream);
 int sparse_max_threads();
+// dense path (pe_dense.hip)
+void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int64_t nArcs,
+                        void* stream);
+int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, const double* Rl,
+                      double* D, int32_t* P, uint8_t* rowActive, uint8_t* rowChanged,
+                      uint8_t* rowAmb, int32_t* dAny, const int32_t* dRows, int32_t nRows,
+                      int64_t n, void* stream, int* sweepsOut);
 
 }  // namespace shdpe

@@ -44,6 +44,16 @@ struct ShdPe {
     bool exactLdsIdx = false;
     int mode = 1;
     std::vector<uint8_t> rowDone;
+    // dense path (mode 3)
+    double* dW = nullptr;
+    double* dRl = nullptr;
+    double* dD = nullptr;
+    int32_t* dP = nullptr;
+    uint8_t* dRowA = nullptr;
+    uint8_t* dRowB = nullptr;
+    uint8_t* dRowAmbD = nullptr;
+    int32_t* dAny = nullptr;
+    int32_t denseRows = 0;
     ShdPeStats stats{};
     std::mutex mu;
 };
@@ -253,6 +263,14 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
     }
     pe->mode = (g.isComplete && pe->opt.forceMode != 1 && pe->opt.forceMode != 3) ? 2 : 1;
     if (pe->opt.forceMode == 2) pe->mode = 2;
+    {
+        // dense non-complete graphs: blocked min-plus (K2)
+        const double density = (double)g.nArcs() / ((double)g.n * (double)g.n);
+        const double dmin = env_double("SHDPE_DENSE_MIN", 0.25);
+        const bool fitsDense = (int64_t)g.n <= 65536;
+        if (pe->mode == 1 && pe->opt.forceMode == 0 && fitsDense && density >= dmin) pe->mode = 3;
+        if (pe->opt.forceMode == 4 && fitsDense) pe->mode = 3;
+    }
     pe->rowDone.assign(T, 0);
     pe->stats.mode = pe->mode;
     pe->stats.isComplete = g.isComplete ? 1 : 0;
@@ -321,6 +339,31 @@ static int ensure_table(ShdPe* pe) {
     return SHD_PE_OK;
 }
 
+static int ensure_dense(ShdPe* pe) {
+    if (pe->dW) return SHD_PE_OK;
+    const int64_t n = pe->hg.n;
+    const int64_t T = (int64_t)pe->attached.size();
+    int rc;
+    void *w, *rl, *d, *p, *ra, *rb, *am, *any;
+    // rows per batch: D (f64) + P (i32) per row
+    const int64_t budget = (int64_t)env_double("SHDPE_DENSE_BATCH_GB", 24.0) * (1LL << 30);
+    int64_t rows = std::max<int64_t>(64, budget / (n * 12));
+    rows = std::min<int64_t>(rows, T);
+    if ((rc = dev_alloc(pe, &w, (size_t)(n * n * 8))) || (rc = dev_alloc(pe, &rl, (size_t)(n * n * 8))) ||
+        (rc = dev_alloc(pe, &d, (size_t)(rows * n * 8))) || (rc = dev_alloc(pe, &p, (size_t)(rows * n * 4))) ||
+        (rc = dev_alloc(pe, &ra, (size_t)rows)) || (rc = dev_alloc(pe, &rb, (size_t)rows)) ||
+        (rc = dev_alloc(pe, &am, (size_t)rows)) || (rc = dev_alloc(pe, &any, 16)))
+        return rc;
+    pe->dW = (double*)w; pe->dRl = (double*)rl; pe->dD = (double*)d; pe->dP = (int32_t*)p;
+    pe->dRowA = (uint8_t*)ra; pe->dRowB = (uint8_t*)rb; pe->dRowAmbD = (uint8_t*)am;
+    pe->dAny = (int32_t*)any;
+    pe->denseRows = (int32_t)rows;
+    launch_dense_build(pe->dg, pe->dW, pe->dRl, n, pe->hg.nArcs(), pe->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(pe->stream));
+    return SHD_PE_OK;
+}
+
 static float elapsed(hipEvent_t a, hipEvent_t b) {
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, a, b);
@@ -351,6 +394,28 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
             pe->stats.launchesDirect++;
         } else if (pe->opt.forceMode == 3) {
             exactRows.assign(pos + c0, pos + c0 + cnt);
+        } else if (pe->mode == 3) {
+            if ((rc = ensure_dense(pe))) return rc;
+            for (int32_t d0 = 0; d0 < cnt; d0 += pe->denseRows) {
+                const int32_t dc = std::min(pe->denseRows, cnt - d0);
+                HIPCHK(hipEventRecord(pe->evA, pe->stream));
+                int sweeps = 0;
+                if (launch_dense_rows(pe->dg, pe->tab, pe->dW, pe->dRl, pe->dD, pe->dP, pe->dRowA,
+                                      pe->dRowB, pe->dRowAmbD, pe->dAny, pe->dRows + d0, dc,
+                                      pe->hg.n, pe->stream, &sweeps))
+                    return SHD_PE_EHIP;
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(pe->evB, pe->stream));
+                amb.resize(dc);
+                HIPCHK(hipMemcpyAsync(amb.data(), pe->dRowAmbD, dc, hipMemcpyDeviceToHost,
+                                      pe->stream));
+                HIPCHK(hipStreamSynchronize(pe->stream));
+                pe->stats.msDenseKernel += elapsed(pe->evA, pe->evB);
+                pe->stats.launchesDense++;
+                pe->stats.denseSweeps += sweeps;
+                for (int32_t i = 0; i < dc; ++i)
+                    if (amb[i]) exactRows.push_back(pos[c0 + d0 + i]);
+            }
         } else {
             HIPCHK(hipEventRecord(pe->evA, pe->stream));
             launch_sparse_rows(pe->dg, pe->tab, pe->sc, pe->dRows, cnt, pe->dRowAmbig, pe->cfg,

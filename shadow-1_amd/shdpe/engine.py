@@ -51,7 +51,9 @@ class Stats(C.Structure):
                 ("msTotal", C.c_double), ("launchesSparse", C.c_int64),
                 ("launchesExact", C.c_int64), ("launchesDirect", C.c_int64),
                 ("mode", C.c_int32), ("isComplete", C.c_int32), ("nVertices", C.c_int32),
-                ("nArcs", C.c_int64), ("nAttached", C.c_int32), ("deltaUsed", C.c_double)]
+                ("nArcs", C.c_int64), ("nAttached", C.c_int32), ("deltaUsed", C.c_double),
+                ("msDenseKernel", C.c_double), ("launchesDense", C.c_int64),
+                ("denseSweeps", C.c_int64)]
 
 
 class EngineError(RuntimeError):

@@ -255,3 +255,26 @@ def test_c2_full_table_properties(E, oracle_mod):
         cand = np.where(coo.row == s, 0.0, lat[coo.row]) + coo.data
         assert np.all(lat[coo.col][coo.col != s] <= cand[coo.col != s])
     eng.close()
+
+
+def test_dense_minplus_shipped_minus_one(E, oracle_mod):
+    """K2 dense path on the shipped graph minus one edge (isComplete FALSE):
+    0.005-quantised latencies -> many tie rows resolved by the exact kernel."""
+    top = Topology.load_npz(os.path.join(GOLDEN, "shipped_topology.npz"))
+    m1 = G.minus_one_edge(top, seed=3)
+    st = _check_engine(E, oracle_mod, m1, np.arange(top.n))
+    assert st["mode"] == 3 and st["launchesDense"] >= 1
+    assert st["rowsExact"] > 0
+
+
+@pytest.mark.parametrize("n,seed", [(700, 3), (1200, 5)])
+def test_dense_minplus_random(E, oracle_mod, n, seed):
+    top = G.dense(n, seed=seed, drop_edge=True)
+    st = _check_engine(E, oracle_mod, top, np.arange(n), sources=np.arange(0, n, 9))
+    assert st["mode"] == 3 and st["denseSweeps"] >= 2
+
+
+def test_dense_forced_on_sparse_graph(E, oracle_mod):
+    top = G.random_sparse(300, 6, seed=44, vloss=True)
+    st = _check_engine(E, oracle_mod, top, np.arange(300), force=4)
+    assert st["mode"] == 3
