@@ -29,6 +29,7 @@ sys.path[:0] = [os.path.join(ROOT, "shadow-1_amd"), os.path.join(ROOT, "oracle")
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TF = 78.6       # MI355X FP64 vector spec
 
 
 def algorithmic_bytes_per_row(n, m_arcs, T):
@@ -143,16 +144,25 @@ def main():
 
     rows_total = T * args.steps
     value = rows_total / elapsed
-    ms_kernel = st["msSparseKernel"] + st["msDirectKernel"]
-    launches = max(1, st["launchesSparse"] + st["launchesDirect"])
+    ms_kernel = st["msSparseKernel"] + st["msDirectKernel"] + st["msDenseKernel"]
+    launches = max(1, st["launchesSparse"] + st["launchesDirect"] + st["launchesDense"])
     avg_launch_ms = ms_kernel / launches
+    bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
     if st["mode"] == 2:
         bytes_per_launch = 36 * T * count
         kname = "k_direct_rows"
+        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    elif st["mode"] == 3:
+        # dense min-plus: FP64 VALU roof, 2*n^2 flops per row per sweep
+        sweeps = st["denseSweeps"] / max(1, st["launchesDense"])
+        bytes_per_launch = 2.0 * n * n * count * (sweeps + 1)       # + predecessor pass
+        kname = "k_minplus_sweep"
+        bound, unit, peak = "valu-fp64", "TFLOP/s", FP64_VALU_PEAK_TF
+        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e12
     else:
         bytes_per_launch = algorithmic_bytes_per_row(n, m_arcs, T) * count
         kname = "k_sparse_rows"
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
     out = {
         "metric": "path-table source rows/sec (latency+reliability)",
@@ -171,10 +181,10 @@ def main():
                    "sources": T, "targets": T, "rows_per_step": T,
                    "parallelism": f"source-row shards x{world}"},
         "edges_relaxed_per_s": m_arcs * rows_total / elapsed,
-        "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        "roofline": {"bound": bound, "kernel": kname, "achieved": achieved,
+                     "peak": peak, "unit": unit, "frac": achieved / peak,
                      "traffic": (traffic or {}).get("bytes_per_launch"),
-                     "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "algorithmic_per_launch": bytes_per_launch,
                      "avg_launch_ms": avg_launch_ms, "launches": launches},
         "rows_exact": st["rowsExact"] // max(1, args.steps),
         "ms_exact_per_step": st["msExactKernel"] / max(1, args.steps),

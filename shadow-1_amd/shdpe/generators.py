@@ -197,7 +197,27 @@ CONFIGS = {
 
 
 def make_config(name: str):
-    """Return (topology, attached) for a named config."""
+    """Return (topology, attached) for a named config.
+
+    c1   shipped topology (complete -> direct rows), 1 host per vertex
+    c1m  shipped topology minus one edge (Dijkstra semantics, tie stress)
+    c2   RGG 10k, all sources        c2q  same, latencies rounded to 0.005
+    c3a  dense 20k complete           c3b  dense 20k minus one edge
+    c4   BA 100k, 16,384 attached     c5   BA 250k, 65,536 attached
+    """
+    if name in ("c1", "c1m"):
+        import os
+        from .graph import Topology
+        here = os.path.dirname(os.path.abspath(__file__))
+        top = Topology.load_npz(os.path.join(here, "..", "..", "tests", "golden",
+                                             "shipped_topology.npz"), name="shipped")
+        if name == "c1m":
+            top = minus_one_edge(top, seed=3)
+        return top, np.arange(top.n, dtype=np.int32)
+    if name in ("c3a", "c3b"):
+        n = int(__import__("os").environ.get("SHDPE_C3_N", "20000"))
+        top = dense(n, seed=3, drop_edge=(name == "c3b"))
+        return top, np.arange(top.n, dtype=np.int32)
     if name == "c2":
         top = rgg(10_000, seed=1)
         return top, np.arange(top.n, dtype=np.int32)
