@@ -78,7 +78,8 @@ typedef struct ShdPeOptions {
     int32_t storePred;       /* keep a predecessor-vertex column in the table      */
     int32_t forceMode;       /* 0 auto, 1 sparse delta-stepping, 2 direct gather,
                                 3 exact igraph-heap kernel for every row (tests),
-                                4 dense blocked min-plus                          */
+                                4 dense blocked min-plus,
+                                5 batched multi-source delta-stepping             */
 } ShdPeOptions;
 
 typedef struct ShdPe ShdPe;

@@ -67,6 +67,29 @@ struct DevScratch {
     int64_t stride;    // elements per slot (>= n)
 };
 
+// Batched multi-source kernel (pe_batch.hip): one slot per resident
+// workgroup; every per-vertex array is [n][LB] (LB sources of the batch
+// side by side, so one arc relaxation serves LB sources with one coalesced
+// access).
+struct BatchScratch {
+    unsigned long long* D;   // [slot][nStride][LB] f64 bit patterns (dist)
+    double* R;               // [slot][nStride][LB] rel product label
+    int32_t* H;              // [slot][nStride][LB] hop label
+    int32_t* P;              // [slot][nStride][LB] chosen IN-arc, -1 none
+    int32_t* X;              // [slot][4][nStride*LB] pointer-jumping / level lists
+    uint32_t* pm;            // [slot][2][nStride] pending lane masks (cur/next)
+    int32_t* queue;          // [slot][nStride] phase candidate list
+    int64_t nStride;         // >= n, multiple of 64
+};
+
+struct BatchLaunch {
+    int32_t lb;              // sources per batch (8 or 16)
+    int32_t threads;         // workgroup size
+    int32_t grid;            // resident workgroups (= scratch slots)
+    int32_t ldsBytes;
+    double delta;            // bucket width
+};
+
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)
 constexpr uint8_t F_UNREACHABLE = 0x01;
 constexpr uint8_t F_NOEDGE = 0x02;
@@ -97,6 +120,14 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
 void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
                         int32_t nRows, void* stream);
 int sparse_max_threads();
+// batched multi-source sparse path (pe_batch.hip): batchRows = nBatches*lb
+// table positions (-1 pads a short batch); rowAmbig[i] = 1 when entry i's
+// row has equal-distance predecessor ties (-> k_exact_rows).
+void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
+                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
+                       const BatchLaunch& cfg, int32_t* dDbg, void* stream);
+const void* batch_kernel_ptr(int lb);
+int batch_lds_bytes(int n);
 // dense path (pe_dense.hip)
 void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int64_t nArcs,
                         void* stream);

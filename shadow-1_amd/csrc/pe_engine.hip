@@ -44,6 +44,14 @@ struct ShdPe {
     bool exactLdsIdx = false;
     int mode = 1;
     std::vector<uint8_t> rowDone;
+    // batched multi-source sparse path (pe_batch.hip)
+    bool batched = false;
+    BatchLaunch bcfg{};
+    BatchScratch bsc{};
+    bool batchReady = false;
+    int32_t* dBatchRows = nullptr;
+    uint8_t* dBatchAmb = nullptr;
+    std::vector<int32_t> rank;        // table position -> BFS visit rank
     // dense path (mode 3)
     double* dW = nullptr;
     double* dRl = nullptr;
@@ -171,6 +179,59 @@ static void configure(ShdPe* pe) {
     int exPerCU = pe->exactLdsIdx ? (int)std::max<long>(1, std::min<long>(8, LDS / std::max<long>(4 * n, 1))) : 8;
     pe->exactGrid = pe->numCUs * exPerCU;
     pe->stats.deltaUsed = c.delta;
+    // Batched multi-source kernel: the layout for graphs whose per-row state
+    // does not fit LDS (LAYOUT 0), or on request (SHDPE_BATCH=1 / forceMode 5).
+    const int wantBatch = env_int("SHDPE_BATCH", -1);
+    pe->batched = wantBatch == 1 || (wantBatch != 0 && layout == 0) || pe->opt.forceMode == 5;
+    BatchLaunch b{};
+    b.lb = env_int("SHDPE_BATCH_LB", 16);
+    if (b.lb != 8 && b.lb != 32) b.lb = 16;
+    b.threads = 1024;
+    b.ldsBytes = batch_lds_bytes((int)n);
+    int bPerCU = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bPerCU, batch_kernel_ptr(b.lb), b.threads,
+                                                     b.ldsBytes) != hipSuccess || bPerCU < 1)
+        bPerCU = 1;
+    b.grid = pe->numCUs * bPerCU;
+    const int gcap = env_int("SHDPE_BATCH_GRID", 0);
+    if (gcap > 0 && gcap < b.grid) b.grid = gcap;
+    const double bf = env_double("SHDPE_BATCH_DELTA_FACTOR", 2.0);
+    b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * bf;
+    if (!(b.delta > 0)) b.delta = 1.0;
+    pe->bcfg = b;
+    if (pe->batched) pe->stats.deltaUsed = b.delta;
+}
+
+// BFS visit rank of every table position (components in vertex order):
+// batches of nearby sources share their delta-stepping frontiers.
+static void compute_ranks(ShdPe* pe) {
+    const HostGraph& g = pe->hg;
+    std::vector<int32_t> order;
+    order.reserve(g.n);
+    std::vector<uint8_t> seen(g.n, 0);
+    for (int32_t r = 0; r < g.n; ++r) {
+        if (seen[r]) continue;
+        seen[r] = 1;
+        size_t head = order.size();
+        order.push_back(r);
+        while (head < order.size()) {
+            const int32_t u = order[head++];
+            for (int32_t a = g.rowPtr[u]; a < g.rowPtr[u + 1]; ++a) {
+                const int32_t v = g.col[a];
+                if (!seen[v]) { seen[v] = 1; order.push_back(v); }
+            }
+            if (g.directed) {
+                for (int32_t a = g.inPtr[u]; a < g.inPtr[u + 1]; ++a) {
+                    const int32_t v = g.inCol[a];
+                    if (!seen[v]) { seen[v] = 1; order.push_back(v); }
+                }
+            }
+        }
+    }
+    pe->rank.assign(pe->attached.size(), 0);
+    int32_t k = 0;
+    for (int32_t v : order)
+        if (pe->posOf[v] >= 0) pe->rank[pe->posOf[v]] = k++;
 }
 
 extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attached,
@@ -272,6 +333,8 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
         if (pe->opt.forceMode == 4 && fitsDense) pe->mode = 3;
     }
     pe->rowDone.assign(T, 0);
+    if (pe->opt.forceMode == 5) pe->mode = 1;
+    if (pe->mode == 1 && pe->batched) compute_ranks(pe);
     pe->stats.mode = pe->mode;
     pe->stats.isComplete = g.isComplete ? 1 : 0;
     pe->stats.nVertices = g.n;
@@ -298,7 +361,7 @@ static int ensure_table(ShdPe* pe) {
     pe->tab.pred = (int32_t*)pred;
     pe->tab.T = (int64_t)T;
     // scratch slots
-    const int slots = std::max(pe->cfg.grid, pe->exactGrid);
+    const int slots = pe->batched ? pe->exactGrid : std::max(pe->cfg.grid, pe->exactGrid);
     const size_t stride = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     void *dist, *sh, *sr, *sp, *hk, *hi, *i2;
     if ((rc = dev_alloc(pe, &dist, slots * stride * 8)) ||
@@ -317,7 +380,7 @@ static int ensure_table(ShdPe* pe) {
     pe->sc.heapIdx = (int32_t*)hi;
     pe->sc.index2 = (int32_t*)i2;
     pe->sc.stride = (int64_t)stride;
-    if (pe->cfg.layout == 3 || pe->cfg.layout == 0) {
+    if (!pe->batched && (pe->cfg.layout == 3 || pe->cfg.layout == 0)) {
         void* q;
         const size_t per = 2 * ((size_t)pe->cfg.qcap + pe->cfg.hcap);
         if ((rc = dev_alloc(pe, &q, (size_t)pe->cfg.grid * per * 4))) return rc;
@@ -336,6 +399,40 @@ static int ensure_table(ShdPe* pe) {
         pe->dDbg = (int32_t*)dbg;
     }
     pe->tableReady = true;
+    return SHD_PE_OK;
+}
+
+static int ensure_batch(ShdPe* pe) {
+    if (pe->batchReady) return SHD_PE_OK;
+    const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
+    const size_t LB = (size_t)pe->bcfg.lb;
+    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4 * 3;
+    // scratch budget (default 64 GiB): fewer resident batches on huge graphs
+    const double budget = env_double("SHDPE_BATCH_SCRATCH_GB", 64.0) * (double)(1ull << 30);
+    const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
+    const size_t nBatchesAll = (pe->attached.size() + LB - 1) / LB;
+    size_t slots = std::min<size_t>({(size_t)pe->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
+    pe->bcfg.grid = (int32_t)slots;
+    int rc;
+    void *D, *R, *H, *P, *X, *pm, *q, *rows, *amb;
+    if ((rc = dev_alloc(pe, &D, slots * NS * LB * 8)) || (rc = dev_alloc(pe, &R, slots * NS * LB * 8)) ||
+        (rc = dev_alloc(pe, &X, slots * NS * LB * 16)) ||
+        (rc = dev_alloc(pe, &H, slots * NS * LB * 4)) || (rc = dev_alloc(pe, &P, slots * NS * LB * 4)) ||
+        (rc = dev_alloc(pe, &pm, slots * NS * 2 * 4)) || (rc = dev_alloc(pe, &q, slots * NS * 4)) ||
+        (rc = dev_alloc(pe, &rows, ((size_t)pe->rowsCap + 64) * 4)) ||
+        (rc = dev_alloc(pe, &amb, (size_t)pe->rowsCap + 64)))
+        return rc;
+    pe->bsc.D = (unsigned long long*)D;
+    pe->bsc.R = (double*)R;
+    pe->bsc.H = (int32_t*)H;
+    pe->bsc.P = (int32_t*)P;
+    pe->bsc.X = (int32_t*)X;
+    pe->bsc.pm = (uint32_t*)pm;
+    pe->bsc.queue = (int32_t*)q;
+    pe->bsc.nStride = (int64_t)NS;
+    pe->dBatchRows = (int32_t*)rows;
+    pe->dBatchAmb = (uint8_t*)amb;
+    pe->batchReady = true;
     return SHD_PE_OK;
 }
 
@@ -415,6 +512,61 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
                 pe->stats.denseSweeps += sweeps;
                 for (int32_t i = 0; i < dc; ++i)
                     if (amb[i]) exactRows.push_back(pos[c0 + d0 + i]);
+            }
+        } else if (pe->batched) {
+            if ((rc = ensure_batch(pe))) return rc;
+            // batches of LB nearby sources (BFS rank order), -1 pads the last
+            const int LB = pe->bcfg.lb;
+            std::vector<int32_t> order(pos + c0, pos + c0 + cnt);
+            std::stable_sort(order.begin(), order.end(),
+                             [&](int32_t a, int32_t b) { return pe->rank[a] < pe->rank[b]; });
+            const int32_t nB = (cnt + LB - 1) / LB;
+            order.resize((size_t)nB * LB, -1);
+            HIPCHK(hipMemcpyAsync(pe->dBatchRows, order.data(), order.size() * 4,
+                                  hipMemcpyHostToDevice, pe->stream));
+            if (pe->dDbg) HIPCHK(hipMemsetAsync(pe->dDbg, 0, (size_t)nB * 64, pe->stream));
+            HIPCHK(hipEventRecord(pe->evA, pe->stream));
+            launch_batch_rows(pe->dg, pe->tab, pe->bsc, pe->dBatchRows, nB, pe->dBatchAmb, pe->bcfg,
+                              pe->dDbg, pe->stream);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(pe->evB, pe->stream));
+            amb.resize(order.size());
+            HIPCHK(hipMemcpyAsync(amb.data(), pe->dBatchAmb, order.size(), hipMemcpyDeviceToHost,
+                                  pe->stream));
+            HIPCHK(hipStreamSynchronize(pe->stream));
+            pe->stats.msSparseKernel += elapsed(pe->evA, pe->evB);
+            pe->stats.launchesSparse++;
+            for (size_t i = 0; i < order.size(); ++i)
+                if (order[i] >= 0 && amb[i]) exactRows.push_back(order[i]);
+            if (pe->dDbg) {
+                std::vector<int32_t> dbg((size_t)nB * 16);
+                HIPCHK(hipMemcpy(dbg.data(), pe->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
+                double ph = 0, pr = 0, kc[5] = {0, 0, 0, 0, 0}, arcsP = 0, lanesP = 0, bmax = 0, bmean = 0, cand = 0;
+                long rnd = 0, dmax = 0, ambB = 0, rep = 0;
+                for (int32_t i = 0; i < nB; ++i) {
+                    const int32_t* d = dbg.data() + 16 * i;
+                    ph += d[0]; rnd += d[1]; dmax = std::max<long>(dmax, d[2]);
+                    ambB += d[3] != 0;
+                    rep += d[15];
+                    pr += d[4];
+                    for (int k = 0; k < 3; ++k) kc[k] += 1024.0 * d[5 + k];
+                    kc[3] += 1024.0 * d[11];
+                    kc[4] += 1024.0 * d[8];
+                    arcsP += 16.0 * d[9];
+                    bmax += 1024.0 * d[12]; bmean += 1024.0 * d[13]; cand += d[14];
+                    lanesP += d[10];
+                }
+                std::fprintf(stderr, "[shdpe] batch relax Mcycles/batch: sum over phases of group-busy max=%.2f mean=%.2f | candidates/batch=%.0f\n",
+                             bmax / nB / 1e6, bmean / nB / 1e6, cand / nB);
+                std::fprintf(stderr, "[shdpe] batch arc-visits/batch=%.0f (%.2f x nArcs) active lanes/proc=%.2f\n",
+                             arcsP / nB, arcsP / nB / (double)pe->hg.nArcs(), lanesP / std::max(pr, 1.0));
+                std::fprintf(stderr, "[shdpe] batch Mcycles/batch: relax=%.2f pred=%.2f "
+                             "depth=%.2f rel=%.2f write=%.2f\n", kc[0] / nB / 1e6, kc[1] / nB / 1e6,
+                             kc[2] / nB / 1e6, kc[3] / nB / 1e6, kc[4] / nB / 1e6);
+                std::fprintf(stderr, "[shdpe] batch LB=%d batches=%d grid=%d delta=%.3f | phases/batch=%.1f "
+                             "vertex-procs/batch=%.0f (%.2f per vertex) | jump rounds/batch=%.1f max depth=%ld amb batches=%ld repairs=%ld\n",
+                             LB, nB, pe->bcfg.grid, pe->bcfg.delta, ph / nB, pr / nB,
+                             pr / nB / pe->hg.n, (double)rnd / nB, dmax, ambB, rep);
             }
         } else {
             HIPCHK(hipEventRecord(pe->evA, pe->stream));

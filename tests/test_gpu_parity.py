@@ -278,3 +278,35 @@ def test_dense_forced_on_sparse_graph(E, oracle_mod):
     top = G.random_sparse(300, 6, seed=44, vloss=True)
     st = _check_engine(E, oracle_mod, top, np.arange(300), force=4)
     assert st["mode"] == 3
+
+
+@pytest.mark.parametrize("case", ["tiefree", "directed", "vloss", "quantized", "power_law",
+                                  "rgg_partial", "missing_loop"])
+def test_batched_kernel(E, oracle_mod, case):
+    """Batched multi-source kernel (forceMode 5, pe_batch.hip) vs the oracle."""
+    if case == "tiefree":
+        top, att, srcs = G.random_sparse(500, 5, seed=201), np.arange(500), None
+    elif case == "directed":
+        top, att, srcs = G.random_sparse(400, 4, seed=202, directed=True), np.arange(400), None
+    elif case == "vloss":
+        top, att, srcs = G.random_sparse(400, 4, seed=203, vloss=True), np.arange(0, 400, 3), None
+    elif case == "quantized":
+        top, att, srcs = G.random_sparse(400, 6, seed=204, quantum=1.0), np.arange(400), None
+    elif case == "power_law":
+        top = G.power_law(6000, m=3, seed=4)
+        att = G.sample_attached(top.n, 1000, seed=2)
+        srcs = att[::7]
+    elif case == "rgg_partial":
+        top = G.rgg(3000, seed=9)
+        att = G.sample_attached(top.n, 700, seed=1)
+        srcs = att[::3]
+    else:
+        src = np.array([0, 1, 2, 3, 0, 2, 3])
+        dst = np.array([1, 2, 0, 0, 0, 2, 3])
+        top = Topology(4, True, src, dst, np.array([1.0, 2.0, 3.0, 4.0, 0.5, 0.5, 0.5]),
+                       np.zeros(7))
+        att, srcs = np.arange(4), None
+    st = _check_engine(E, oracle_mod, top, att, sources=srcs, force=5)
+    assert st["mode"] == 1 and st["launchesSparse"] >= 1
+    if case == "quantized":
+        assert st["rowsExact"] > 0
