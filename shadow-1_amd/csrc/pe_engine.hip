@@ -195,7 +195,7 @@ static void configure(ShdPe* pe) {
     b.grid = pe->numCUs * bPerCU;
     const int gcap = env_int("SHDPE_BATCH_GRID", 0);
     if (gcap > 0 && gcap < b.grid) b.grid = gcap;
-    const double bf = env_double("SHDPE_BATCH_DELTA_FACTOR", 2.0);
+    const double bf = env_double("SHDPE_BATCH_DELTA_FACTOR", 8.0);
     b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * bf;
     if (!(b.delta > 0)) b.delta = 1.0;
     pe->bcfg = b;

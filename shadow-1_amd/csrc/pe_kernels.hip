@@ -88,7 +88,9 @@ __device__ __noinline__ double fold_rel_general(const DevGraph& g, const int32_t
 
 // Row writer shared by the sparse and exact kernels (topology.c:1805-1864).
 // Targets are processed in groups of 4 so their independent loads overlap.
-template <class DistOf, class HopOf>
+// NT_OUT: streaming (nontemporal) stores, so the table stream does not evict
+// the L2-resident graph.
+template <bool NT_OUT = false, class DistOf, class HopOf>
 __device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab, int r, int s,
                                          DistOf distOf, HopOf hopOf, const double* R,
                                          const int32_t* P, uint8_t extra, int tid, int NT) {
@@ -147,18 +149,30 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab
                     f |= F_ZEROLAT;
                 }
             }
-            oLat[j] = L;
-            oRel[j] = Rl;
-            oHops[j] = h;
-            oFlags[j] = f;
-            if (oPred) oPred[j] = pv;
+            if (NT_OUT) {
+                __builtin_nontemporal_store(L, &oLat[j]);
+                __builtin_nontemporal_store(Rl, &oRel[j]);
+                __builtin_nontemporal_store(h, &oHops[j]);
+                __builtin_nontemporal_store(f, &oFlags[j]);
+                if (oPred) __builtin_nontemporal_store(pv, &oPred[j]);
+            } else {
+                oLat[j] = L;
+                oRel[j] = Rl;
+                oHops[j] = h;
+                oFlags[j] = f;
+                if (oPred) oPred[j] = pv;
+            }
         }
     }
 }
 
 constexpr int UNR = 8;   // arcs loaded per batch (independent loads in flight)
-constexpr int LPV = 4;   // lanes per light frontier vertex
-constexpr int UNRG = 4;  // arcs preloaded per lane per batch
+// lanes per light frontier vertex: template parameter LPVL of k_sparse_rows
+// (4 by default; kflags bits 4-5 select 2 / 1 / 8 for tuning).  Each group
+// preloads 16 arcs per batch (UNRG per lane) so a degree <= 16 vertex needs
+// one round of independent loads.
+template <int LPV>
+struct Unr { static constexpr int value = LPV <= 16 ? 16 / LPV : 4; };
 
 // Per-row state placement.  LAYOUT 2: dist, hops (u16), rowPtr in LDS;
 // LAYOUT 1: dist in LDS; LAYOUT 0: everything in the workgroup's HBM slot.
@@ -212,6 +226,7 @@ template <int LPV, int LAYOUT, bool QUEUED>
 __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LAYOUT>& c, int u,
                                               int s, int sub, int kflags,
                                               long long* st = nullptr) {
+    constexpr int UNRG = Unr<LPV>::value;
     long long p0 = st ? clock64() : 0;
     unsigned long long best = INF_BITS;
     int cnt = 0, ba = -1, bh = 0;   // ba: chosen in-arc, bh: its tail vertex
@@ -224,23 +239,40 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
         const double du = b2d(dub);
         const int a0 = c.rp[u], a1 = c.rp[u + 1];
         for (int ab = a0 + sub; ab < a1; ab += LPV * UNRG) {
+            // Branch-free batch: out-of-range slots re-load arc ab (valid,
+            // since ab < a1) and are masked afterwards, so every load of the
+            // batch is in flight before the first wait (a branch per slot
+            // makes the waitcnt pass serialise them).
             int xs[UNRG];
             double ws[UNRG];
             unsigned long long dx[UNRG];
+            bool ok[UNRG];
+            if (kflags & 1) {
 #pragma unroll
-            for (int k = 0; k < UNRG; ++k) {
-                const int a = ab + k * LPV;
-                if (a < a1) {
-                    if (kflags & 1) { const Arc A = g.arcs[a]; xs[k] = A.col; ws[k] = A.lat; }
-                    else { xs[k] = g.col[a]; ws[k] = g.lat[a]; }
-                } else xs[k] = -1;
+                for (int k = 0; k < UNRG; ++k) {
+                    const int a = ab + k * LPV;
+                    ok[k] = a < a1;
+                    const int ac = ok[k] ? a : ab;
+                    xs[k] = g.col[ac];
+                    ws[k] = g.lat[ac];
+                }
+            } else {
+                // one 16-B request per arc (lat f64 | col i32); the LPV lanes
+                // of a group read consecutive arcs -> one line per group
+#pragma unroll
+                for (int k = 0; k < UNRG; ++k) {
+                    const int a = ab + k * LPV;
+                    ok[k] = a < a1;
+                    const Arc A = g.arcs[ok[k] ? a : ab];
+                    xs[k] = A.col;
+                    ws[k] = A.lat;
+                }
             }
 #pragma unroll
-            for (int k = 0; k < UNRG; ++k)
-                if (xs[k] >= 0) dx[k] = ld_relaxed(&c.dist[xs[k]]);
+            for (int k = 0; k < UNRG; ++k) dx[k] = ld_relaxed(&c.dist[xs[k]]);
 #pragma unroll
             for (int k = 0; k < UNRG; ++k) {
-                if (xs[k] < 0) continue;
+                if (!ok[k]) continue;
                 const int x = xs[k];
                 const unsigned long long dxb = dx[k];
                 if (undirected && dxb < dub && b2d(dxb) + ws[k] == du) {
@@ -316,7 +348,7 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
 // ---------------------------------------------------------------------------
 // k_sparse_rows
 // ---------------------------------------------------------------------------
-template <int LAYOUT>
+template <int LAYOUT, int LPV>
 __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
     DevGraph g0, DevTable tab0, DevScratch sc0, const int32_t* __restrict__ rows, int32_t nRows,
     uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg, int32_t* dbg,
@@ -658,41 +690,109 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
         // unless two distinct vertices tie on that minimum (then the heap's
         // pop order decides -> row goes to k_exact_rows).
         int myAmb = 0, myMis = 0;
-        for (int v = tid; v < n; v += NT) {
-            if (v == s) continue;
-            const unsigned long long dvb = c.dist[v];
-            if (dvb == INF_BITS) { c.P[v] = -1; continue; }
-            const double dv = b2d(dvb);
-            unsigned long long best = INF_BITS;
-            int cnt = 0, ba = -1, bu = -1;
-            const bool undirected = g.inCol == g.col;
-            const int a0 = undirected ? c.rp[v] : g.inPtr[v];
-            const int a1 = undirected ? c.rp[v + 1] : g.inPtr[v + 1];
-            for (int a = a0; a < a1; a += UNR) {
-                int cu[UNR];
-                double lw[UNR];
-#pragma unroll
-                for (int k = 0; k < UNR; ++k) {
-                    if (a + k < a1) {
-                        if (undirected && (kflags & 2)) { const Arc A = g.arcs[a + k]; cu[k] = A.col; lw[k] = A.lat; }
-                        else { cu[k] = g.inCol[a + k]; lw[k] = g.inLat[a + k]; }
+        if (!(kflags & 8)) {
+            for (int v = tid; v < n; v += NT) {
+                if (v == s) continue;
+                const unsigned long long dvb = c.dist[v];
+                if (dvb == INF_BITS) { c.P[v] = -1; continue; }
+                const double dv = b2d(dvb);
+                unsigned long long best = INF_BITS;
+                int cnt = 0, ba = -1, bu = -1;
+                const bool undirected = g.inCol == g.col;
+                const int a0 = undirected ? c.rp[v] : g.inPtr[v];
+                const int a1 = undirected ? c.rp[v + 1] : g.inPtr[v + 1];
+                for (int a = a0; a < a1; a += UNR) {
+                    int cu[UNR];
+                    double lw[UNR];
+                    unsigned long long du[UNR];
+    #pragma unroll
+                    for (int k = 0; k < UNR; ++k) {       // branch-free (see process_group)
+                        const int ac = a + k < a1 ? a + k : a;
+                        cu[k] = g.inCol[ac];
+                        lw[k] = g.inLat[ac];
                     }
-                }
-#pragma unroll
-                for (int k = 0; k < UNR; ++k) {
-                    if (a + k < a1) {
-                        const unsigned long long dub = c.dist[cu[k]];
-                        if (dub <= dvb && b2d(dub) + lw[k] == dv) {
-                            if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
-                            if (dub < best) { best = dub; cnt = 1; ba = a + k; bu = cu[k]; }
-                            else if (dub == best) ++cnt;
+    #pragma unroll
+                    for (int k = 0; k < UNR; ++k) du[k] = c.dist[cu[k]];
+    #pragma unroll
+                    for (int k = 0; k < UNR; ++k) {
+                        if (a + k < a1) {
+                            const unsigned long long dub = du[k];
+                            if (dub <= dvb && b2d(dub) + lw[k] == dv) {
+                                if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
+                                if (dub < best) { best = dub; cnt = 1; ba = a + k; bu = cu[k]; }
+                                else if (dub == best) ++cnt;
+                            }
                         }
                     }
                 }
+                if (cnt != 1) { myAmb = 1; if (ba < 0) { c.P[v] = -1; continue; } }
+                c.P[v] = ba;
+                if ((int)c.H[v] != (int)c.H[bu] + 1 || c.R[v] != c.R[bu] * g.inRel[ba]) myMis = 1;
             }
-            if (cnt != 1) { myAmb = 1; if (ba < 0) { c.P[v] = -1; continue; } }
-            c.P[v] = ba;
-            if ((int)c.H[v] != (int)c.H[bu] + 1 || c.R[v] != c.R[bu] * g.inRel[ba]) myMis = 1;
+        } else {
+            // Grouped variant (kflags & 8; measured slower on C2, kept for
+            // tuning): PL lanes per vertex read consecutive in-arcs (one line
+            // per group per request instead of one per lane), PL*PU arcs per
+            // batch, then a DPP merge of (min dist[u], count, first arc).
+            constexpr int PL = 4, PU = 4;
+            const int grp = tid / PL, sub = tid % PL, NG = NT / PL;
+            const bool undirected = g.inCol == g.col;
+            for (int v0 = 0; v0 < n; v0 += NG) {
+                const int v = v0 + grp;
+                const bool inV = v < n && v != s;
+                const unsigned long long dvb = inV ? c.dist[v] : INF_BITS;
+                const bool act = dvb != INF_BITS;
+                const double dv = b2d(dvb);
+                unsigned long long best = INF_BITS;
+                int cnt = 0, ba = -1, bu = -1;
+                if (act) {
+                    const int a0 = undirected ? c.rp[v] : g.inPtr[v];
+                    const int a1 = undirected ? c.rp[v + 1] : g.inPtr[v + 1];
+                    for (int ab = a0 + sub; ab < a1; ab += PL * PU) {
+                        int cu[PU];
+                        double lw[PU];
+                        unsigned long long du[PU];
+                        bool ok[PU];
+#pragma unroll
+                        for (int k = 0; k < PU; ++k) {
+                            const int a = ab + k * PL;
+                            ok[k] = a < a1;
+                            const int ac = ok[k] ? a : ab;
+                            if (undirected) { const Arc A = g.arcs[ac]; cu[k] = A.col; lw[k] = A.lat; }
+                            else { cu[k] = g.inCol[ac]; lw[k] = g.inLat[ac]; }
+                        }
+#pragma unroll
+                        for (int k = 0; k < PU; ++k) du[k] = c.dist[cu[k]];
+#pragma unroll
+                        for (int k = 0; k < PU; ++k) {
+                            if (!ok[k]) continue;
+                            const unsigned long long dub = du[k];
+                            if (dub <= dvb && b2d(dub) + lw[k] == dv) {
+                                if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
+                                if (dub < best) { best = dub; cnt = 1; ba = ab + k * PL; bu = cu[k]; }
+                                else if (dub == best) ++cnt;
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int o = PL >> 1; o > 0; o >>= 1) {
+                    const unsigned long long ob = gxor64<PL>(best, o);
+                    const int oc = gxor<PL>(cnt, o);
+                    const int oa = gxor<PL>(ba, o);
+                    const int ou = gxor<PL>(bu, o);
+                    if (ob < best) { best = ob; cnt = oc; ba = oa; bu = ou; }
+                    else if (ob == best && oa >= 0) {
+                        cnt += oc;
+                        if (ba < 0 || oa < ba) { ba = oa; bu = ou; }
+                    }
+                }
+                if (sub != 0 || !inV) continue;
+                if (!act) { c.P[v] = -1; continue; }
+                if (cnt != 1) { myAmb = 1; if (ba < 0) { c.P[v] = -1; continue; } }
+                c.P[v] = ba;
+                if ((int)c.H[v] != (int)c.H[bu] + 1 || c.R[v] != c.R[bu] * g.inRel[ba]) myMis = 1;
+            }
         }
         if (myAmb) atomicOr(&ctl->ambig, 1);
         if (myMis) atomicOr(&ctl->mismatch, 1);
@@ -747,8 +847,12 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
             if (dbg) dbg[16 * b + 1] = jac;
         }
         const long long tW = clock64();
-        write_row(g, tab, r, s, [&](int t) { return c.dist[t]; },
-                  [&](int t) { return (int)c.H[t]; }, c.R, c.P, 0, tid, NT);
+        if (kflags & 4)
+            write_row<true>(g, tab, r, s, [&](int t) { return c.dist[t]; },
+                            [&](int t) { return (int)c.H[t]; }, c.R, c.P, 0, tid, NT);
+        else
+            write_row(g, tab, r, s, [&](int t) { return c.dist[t]; },
+                      [&](int t) { return (int)c.H[t]; }, c.R, c.P, 0, tid, NT);
         __syncthreads();
         if (dbg && tid == 0) dbg[16 * b + 7] = (int)((clock64() - tW) >> 4);
     }
@@ -952,15 +1056,31 @@ __global__ __launch_bounds__(256) void k_direct_rows(DevGraph g0, DevTable tab0,
 // ---------------------------------------------------------------------------
 int sparse_max_threads() { return SP_THREADS; }
 
+template <int L, int LPV>
+static void launch_sparse_lpv(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                              const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
+                              const SparseLaunch& cfg, int32_t* dDbg, hipStream_t st, int grid) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<L, LPV>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
+    hipLaunchKernelGGL((k_sparse_rows<L, LPV>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st,
+                       g, tab, sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap,
+                       cfg.heavyDeg, dDbg, cfg.kflags);
+}
+
 template <int L>
 static void launch_sparse_layout(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                                  const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
                                  const SparseLaunch& cfg, int32_t* dDbg, hipStream_t st, int grid) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<L>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-    hipLaunchKernelGGL(k_sparse_rows<L>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
-                       sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap, cfg.heavyDeg,
-                       dDbg, cfg.kflags);
+    if constexpr (L == 3) {
+        const int sel = (cfg.kflags >> 4) & 3;
+        if (sel == 1)
+            return launch_sparse_lpv<L, 2>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+        if (sel == 2)
+            return launch_sparse_lpv<L, 1>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+        if (sel == 3)
+            return launch_sparse_lpv<L, 8>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+    }
+    launch_sparse_lpv<L, 4>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
 }
 
 void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
