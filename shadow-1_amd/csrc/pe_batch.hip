@@ -203,17 +203,19 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                 int u[BV], a0[BV], a1[BV];
                 unsigned long long db[BV], dub[BV];
 #pragma unroll
-                for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? ld_wg(&Q[i0 + v]) : -1;
+                for (int v = 0; v < BV; ++v) {
+                    const int uq = ld_wg(&Q[i0 + v < qn ? i0 + v : i0]);
+                    u[v] = i0 + v < qn ? uq : -1;
+                }
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    if (u[v] >= 0) {
-                        db[v] = ld_wg(&D[(size_t)u[v] * LB + l]);
-                        a0[v] = g.rowPtr[u[v]];          // same round trip as dist[u]
-                        a1[v] = g.rowPtr[u[v] + 1];
-                    } else {
-                        db[v] = INF_BITS;
-                        a0[v] = a1[v] = 0;
-                    }
+                    // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
+                    const int uc = u[v] >= 0 ? u[v] : 0;
+                    const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                    const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
+                    db[v] = u[v] >= 0 ? d0 : INF_BITS;
+                    a0[v] = u[v] >= 0 ? r0 : 0;
+                    a1[v] = u[v] >= 0 ? r1 : 0;
                 }
                 int maxd = 0;
 #pragma unroll
@@ -238,25 +240,24 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                     int xs[BV][BK];
                     double ws[BV][BK];
                     unsigned long long dx[BV][BK];
+                    // branch-free: out-of-range slots load arc 0 / vertex 0
+                    // and are masked, so all BV*BK loads of a stage are in
+                    // flight before the first wait
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const int a = a0[v] + t + k;
-                            if (a < a1[v]) {
-                                const Arc A = g.arcs[a];
-                                xs[v][k] = A.col;
-                                ws[v][k] = A.lat;
-                            } else {
-                                xs[v][k] = -1;
-                                ws[v][k] = 0.0;
-                            }
+                            const bool ok = a < a1[v];
+                            const Arc A = g.arcs[ok ? a : 0];
+                            xs[v][k] = ok ? A.col : -1;
+                            ws[v][k] = A.lat;
                         }
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[v][k] = xs[v][k] >= 0 ? ld_wg(&D[(size_t)xs[v][k] * LB + l]) : 0ull;
+                            dx[v][k] = ld_wg(&D[(size_t)(xs[v][k] >= 0 ? xs[v][k] : 0) * LB + l]);
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
@@ -358,27 +359,29 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
-                        for (int k = 0; k < BK; ++k) {
+                        for (int k = 0; k < BK; ++k) {      // branch-free (see pass 1)
                             const int a = a0[v] + t + k;
-                            if (a < a1[v]) {
-                                if (undirected) {
-                                    const Arc A = g.arcs[a];
-                                    cu[v][k] = A.col;
-                                    lw[v][k] = A.lat;
-                                } else {
-                                    cu[v][k] = g.inCol[a];
-                                    lw[v][k] = g.inLat[a];
-                                }
+                            const bool ok = a < a1[v];
+                            const int ac = ok ? a : 0;
+                            int c;
+                            if (undirected) {
+                                const Arc A = g.arcs[ac];
+                                c = A.col;
+                                lw[v][k] = A.lat;
                             } else {
-                                cu[v][k] = -1;
-                                lw[v][k] = 0.0;
+                                c = g.inCol[ac];
+                                lw[v][k] = g.inLat[ac];
                             }
+                            cu[v][k] = ok ? c : -1;
                         }
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
-                        for (int k = 0; k < BK; ++k)
-                            du[v][k] = cu[v][k] >= 0 ? ld_wg(&D[(size_t)cu[v][k] * LB + l]) : INF_BITS;
+                        for (int k = 0; k < BK; ++k) {
+                            const unsigned long long t2 =
+                                ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]);
+                            du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
+                        }
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
