@@ -55,13 +55,21 @@ struct DevTable {
     int64_t T;
 };
 
+// k_exact_rows heap entry (igraph_2wheap_t data + index, labels alongside)
+struct alignas(8) XEnt {
+    double key;
+    double rel;
+    int32_t idx;
+    int32_t hops;
+};
+
 struct DevScratch {
     double* dist;      // exact kernel: final distance at pop
     int32_t* hops;
     double* rel;
     int32_t* pred;     // IN-arc index of the chosen predecessor edge, -1 none
-    double* heapKey;   // exact kernel 2-way heap (igraph_2wheap_t data)
-    int32_t* heapIdx;  // exact kernel 2-way heap (index)
+    XEnt* heapEnt;     // exact kernel 2-way heap entries at positions >= hc (LDS below)
+    int64_t heapStride;  // entries per slot in heapEnt
     int32_t* index2;   // exact kernel: 0 never reached, 1 popped, >=2 heap pos+2
     int32_t* queue;    // sparse LAYOUT 3: frontier queues, (stride + hcap) per slot
     int64_t stride;    // elements per slot (>= n)
@@ -115,8 +123,8 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
                         const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
                         const SparseLaunch& cfg, int32_t* dDbg, void* stream);
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
-                       const int32_t* dRows, int32_t nRows, int32_t grid, bool ldsIndex,
-                       void* stream);
+                       const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
+                       bool ldsIndex, void* stream);
 void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
                         int32_t nRows, void* stream);
 int sparse_max_threads();

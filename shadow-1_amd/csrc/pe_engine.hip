@@ -41,6 +41,7 @@ struct ShdPe {
     int32_t rowsCap = 0;
     SparseLaunch cfg{};
     int exactGrid = 0;
+    int exactHc = 1;
     bool exactLdsIdx = false;
     int mode = 1;
     std::vector<uint8_t> rowDone;
@@ -175,9 +176,17 @@ static void configure(ShdPe* pe) {
     if (!(c.delta > 0)) c.delta = 1.0;
     c.kflags = env_int("SHDPE_KFLAGS", 0);
     pe->cfg = c;
-    pe->exactLdsIdx = (size_t)4 * n <= 64 * 1024;
-    int exPerCU = pe->exactLdsIdx ? (int)std::max<long>(1, std::min<long>(8, LDS / std::max<long>(4 * n, 1))) : 8;
-    pe->exactGrid = pe->numCUs * exPerCU;
+    // k_exact_rows: index2 (4n) in LDS up to n = 24k, heap entries (24 B)
+    // in LDS up to the budget, the tail of the heap in the global slot.  A
+    // whole heap that fits leaves room for several rows per CU.
+    pe->exactLdsIdx = (size_t)4 * n <= 96 * 1024;
+    const long idxB = pe->exactLdsIdx ? 4 * n : 0;
+    const long perWG = std::min<long>(LDS, idxB + 24 * n + 16);
+    pe->exactHc = (int)std::max<long>(1, std::min<long>(n, (perWG - idxB - 16) / 24));
+    const int hcCap = env_int("SHDPE_EXACT_HC", 0);   // testing: force the global heap tail
+    if (hcCap > 0) pe->exactHc = std::min(pe->exactHc, hcCap);
+    const int exPerCU = (int)std::max<long>(1, std::min<long>(8, LDS / perWG));
+    pe->exactGrid = pe->numCUs * env_int("SHDPE_EXACT_PER_CU", exPerCU);
     pe->stats.deltaUsed = c.delta;
     // Batched multi-source kernel: the layout for graphs whose per-row state
     // does not fit LDS (LAYOUT 0), or on request (SHDPE_BATCH=1 / forceMode 5).
@@ -363,21 +372,21 @@ static int ensure_table(ShdPe* pe) {
     // scratch slots
     const int slots = pe->batched ? pe->exactGrid : std::max(pe->cfg.grid, pe->exactGrid);
     const size_t stride = ((size_t)pe->hg.n + 63) & ~(size_t)63;
-    void *dist, *sh, *sr, *sp, *hk, *hi, *i2;
+    const size_t heapStride = std::max<size_t>(1, (size_t)pe->hg.n - (size_t)pe->exactHc);
+    void *dist, *sh, *sr, *sp, *hk, *i2;
     if ((rc = dev_alloc(pe, &dist, slots * stride * 8)) ||
         (rc = dev_alloc(pe, &sh, slots * stride * 4)) ||
         (rc = dev_alloc(pe, &sr, slots * stride * 8)) ||
         (rc = dev_alloc(pe, &sp, slots * stride * 4)) ||
-        (rc = dev_alloc(pe, &hk, (size_t)pe->exactGrid * stride * 8)) ||
-        (rc = dev_alloc(pe, &hi, (size_t)pe->exactGrid * stride * 4)) ||
+        (rc = dev_alloc(pe, &hk, (size_t)pe->exactGrid * heapStride * sizeof(XEnt))) ||
         (rc = dev_alloc(pe, &i2, pe->exactLdsIdx ? 16 : (size_t)pe->exactGrid * stride * 4)))
         return rc;
     pe->sc.dist = (double*)dist;
     pe->sc.hops = (int32_t*)sh;
     pe->sc.rel = (double*)sr;
     pe->sc.pred = (int32_t*)sp;
-    pe->sc.heapKey = (double*)hk;
-    pe->sc.heapIdx = (int32_t*)hi;
+    pe->sc.heapEnt = (XEnt*)hk;
+    pe->sc.heapStride = (int64_t)heapStride;
     pe->sc.index2 = (int32_t*)i2;
     pe->sc.stride = (int64_t)stride;
     if (!pe->batched && (pe->cfg.layout == 3 || pe->cfg.layout == 0)) {
@@ -621,7 +630,7 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
                                   hipMemcpyHostToDevice, pe->stream));
             HIPCHK(hipEventRecord(pe->evA, pe->stream));
             launch_exact_rows(pe->dg, pe->tab, pe->sc, pe->dRows, (int32_t)exactRows.size(),
-                              pe->exactGrid, pe->exactLdsIdx, pe->stream);
+                              pe->exactGrid, pe->exactHc, pe->exactLdsIdx, pe->stream);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(pe->evB, pe->stream));
             HIPCHK(hipEventSynchronize(pe->evB));

@@ -62,17 +62,21 @@ static_assert(sizeof(Ctrl) <= 64, "ctrl block");
 // Forward fold of reliability with vertex factors (topology.c:1430-1462,
 // :1499) for entries where a_s * a_t != 1: walk the chosen predecessor chain
 // back to s, then multiply in source->target order.
-__device__ __noinline__ double fold_rel_general(const DevGraph& g, const int32_t* P, int s, int t,
-                                                int h) {
-    double acc = 1.0 * g.vrel[s];
-    acc = acc * g.vrel[t];
+// (Arrays passed by value: a DevGraph& to a non-inlined callee would force
+// the caller's graph descriptor into scratch memory.)
+__device__ __noinline__ double fold_rel_general(const double* __restrict__ vrel,
+                                                const double* __restrict__ inRel,
+                                                const int32_t* __restrict__ inCol,
+                                                const int32_t* P, int s, int t, int h) {
+    double acc = 1.0 * vrel[s];
+    acc = acc * vrel[t];
     if (h <= 64) {
         double fac[64];
         int k = 0, x = t;
         while (x != s && k < 64) {
             int a = P[x];
-            fac[k++] = g.inRel[a];
-            x = g.inCol[a];
+            fac[k++] = inRel[a];
+            x = inCol[a];
         }
         for (int i = k - 1; i >= 0; --i) acc = acc * fac[i];
         return acc;
@@ -80,8 +84,8 @@ __device__ __noinline__ double fold_rel_general(const DevGraph& g, const int32_t
     // long chains: O(h^2) re-walk, exact order, no scratch
     for (int d = 1; d <= h; ++d) {
         int x = t;
-        for (int up = 0; up < h - d; ++up) x = g.inCol[P[x]];
-        acc = acc * g.inRel[P[x]];
+        for (int up = 0; up < h - d; ++up) x = inCol[P[x]];
+        acc = acc * inRel[P[x]];
     }
     return acc;
 }
@@ -143,7 +147,7 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab
                 h = hh[k];
                 if (oPred) pv = g.inCol[pa[k]];
                 if (g.vrel[s] == 1.0 && g.vrel[t] == 1.0) Rl = rr[k];
-                else Rl = fold_rel_general(g, P, s, t, h);
+                else Rl = fold_rel_general(g.vrel, g.inRel, g.inCol, P, s, t, h);
                 if (L == 0.0) {                    // topology.c:1848-1852
                     L = 1.0;
                     f |= F_ZEROLAT;
@@ -861,148 +865,239 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
 // ---------------------------------------------------------------------------
 // k_exact_rows: igraph 0.7.1 Dijkstra with the 2-way heap (heap.c), one wave
 // per row.  index2: 0 never reached, 1 popped, >=2 heap position + 2.
+//
+// The heap is an array of 24-B entries {key, rel, idx, hops} (the labels
+// ride along, so a pop needs no label gather); positions < hc live in LDS,
+// the rest in the workgroup's global slot.  Lane 0 owns the heap and moves
+// a hole instead of swapping (sift-down/up with the moving key in a
+// register: one LDS round trip per level); the end state is identical to
+// igraph's swap-based igraph_i_2wheap_sink / _shift_up, so the pop order is
+// too.  The wave pre-checks all arcs of the popped vertex in parallel (the
+// decision for arc k depends only on v_k's own state: no parallel edges, no
+// self-loops in the CSR), writes the labels, and lane 0 then applies the
+// pushes / modifies serially in incidence order.  rowPtr of the next top is
+// fetched before the pop's sift-down.
 // ---------------------------------------------------------------------------
+static_assert(sizeof(XEnt) == 24, "heap entry");
+
+// Heap storage: positions < hc in LDS (dynamic shared memory at offset 0,
+// addressed through the __shared__ symbol so accesses stay ds_* -- a flat
+// access would also wait for every outstanding global store), the tail in
+// the global slot.  index2 in LDS after the heap (LDSIDX) or global.
+extern __shared__ __attribute__((aligned(16))) unsigned char ex_smem[];
+
+template <bool LDSIDX>
 struct XHeap {
-    double* key;
-    int32_t* idx;
-    int32_t* index2;
+    XEnt* glb;        // global tail (position p >= hc at glb[p - hc])
+    int32_t* gidx;    // global index2 (!LDSIDX)
+    int hc;
     int size;
-};
-
-__device__ __forceinline__ void xh_switch(XHeap& h, int e1, int e2) {
-    if (e1 != e2) {
-        const double t3 = h.key[e1];
-        h.key[e1] = h.key[e2];
-        h.key[e2] = t3;
-        const int t1 = h.idx[e1], t2 = h.idx[e2];
-        h.index2[t1] = e2 + 2;
-        h.index2[t2] = e1 + 2;
-        h.idx[e1] = t2;
-        h.idx[e2] = t1;
+    __device__ __forceinline__ int32_t* lidx() const {
+        return reinterpret_cast<int32_t*>(ex_smem + (size_t)24 * hc);
     }
-}
-
-__device__ void xh_shift_up(XHeap& h, int elem) {
-    while (!(elem == 0 || h.key[elem] < h.key[((elem + 1) >> 1) - 1])) {
-        const int p = ((elem + 1) >> 1) - 1;
-        xh_switch(h, elem, p);
-        elem = p;
+    __device__ __forceinline__ int32_t idx2(int v) const { return LDSIDX ? lidx()[v] : gidx[v]; }
+    __device__ __forceinline__ void set_idx2(int v, int x) const {
+        if (LDSIDX) lidx()[v] = x; else gidx[v] = x;
     }
-}
-
-__device__ void xh_sink(XHeap& h, int head) {
-    for (;;) {
-        const int l = (head + 1) * 2 - 1, rr = (head + 1) * 2;
-        if (l >= h.size) return;
-        if (rr == h.size || h.key[l] >= h.key[rr]) {
-            if (h.key[head] < h.key[l]) { xh_switch(h, head, l); head = l; }
-            else return;
+    // any lane (pre-check): LDS read always, global only for tail positions
+    __device__ __forceinline__ double key(int p) const {
+        if (p < hc) return reinterpret_cast<const XEnt*>(ex_smem)[p].key;
+        double k = glb[p - hc].key;
+        asm volatile("" : "+v"(k));
+        return k;
+    }
+    // lane 0 only: p is made scalar so the LDS/global choice is a uniform
+    // branch (a per-lane select would become one flat access)
+    __device__ __forceinline__ XEnt load(int p) const {
+        p = __builtin_amdgcn_readfirstlane(p);
+        if (p < hc) return reinterpret_cast<const XEnt*>(ex_smem)[p];
+        XEnt e = glb[p - hc];
+        asm volatile("" : "+v"(e.key));   // keeps the two loads apart (no flat merge)
+        return e;
+    }
+    __device__ __forceinline__ void place(int p, const XEnt& e) const {
+        p = __builtin_amdgcn_readfirstlane(p);
+        if (p < hc) {
+            reinterpret_cast<XEnt*>(ex_smem)[p] = e;
         } else {
-            if (h.key[head] < h.key[rr]) { xh_switch(h, head, rr); head = rr; }
-            else return;
+            glb[p - hc] = e;
+            asm volatile("" ::: "memory");
+        }
+        set_idx2(e.idx, p + 2);
+    }
+    // igraph_i_2wheap_sink: go left when left >= right (or no right child),
+    // move only if the moving key is strictly smaller.  Returns the hole.
+    __device__ __forceinline__ int sink_hole(int head, double k) const {
+        for (;;) {
+            const int l = 2 * head + 1, r = l + 1;
+            if (l >= size) return head;
+            const XEnt L = load(l);
+            const bool hasR = r < size;
+            const XEnt R = load(hasR ? r : l);
+            const bool useL = !hasR || L.key >= R.key;
+            XEnt C;
+            C.key = useL ? L.key : R.key;
+            C.rel = useL ? L.rel : R.rel;
+            C.idx = useL ? L.idx : R.idx;
+            C.hops = useL ? L.hops : R.hops;
+            if (!(k < C.key)) return head;
+            place(head, C);
+            head = useL ? l : r;
         }
     }
-}
+    // igraph_i_2wheap_shift_up: rise unless strictly smaller than the parent
+    // (equal keys rise above existing ones).
+    __device__ __forceinline__ void shift_up_place(int elem, const XEnt& e) const {
+        while (elem > 0) {
+            const int p = ((elem + 1) >> 1) - 1;
+            const XEnt P = load(p);
+            if (e.key < P.key) break;
+            place(elem, P);
+            elem = p;
+        }
+        place(elem, e);
+    }
+};
 
-__device__ __forceinline__ void xh_push(XHeap& h, int v, double k) {
-    const int sz = h.size;
-    h.key[sz] = k;
-    h.idx[sz] = v;
-    h.size = sz + 1;
-    h.index2[v] = sz + 2;
-    xh_shift_up(h, sz);
-}
-
-__device__ __forceinline__ void xh_modify(XHeap& h, int v, double k) {
-    const int pos = h.index2[v] - 2;
-    h.key[pos] = k;
-    xh_sink(h, pos);
-    xh_shift_up(h, pos);
+// Stream an array through the cache hierarchy once (16-B loads, 8 in flight
+// per lane): the exact kernel touches each vertex's arcs once per row in a
+// dependent chain, so without this every pop pays HBM latency twice.
+__device__ __forceinline__ uint32_t warm_cache(const void* p, size_t bytes, int lane, int nl) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const size_t nv = bytes / 16;
+    uint32_t acc = 0;
+    for (size_t i = lane; i < nv; i += (size_t)nl * 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const size_t j = i + (size_t)k * nl;
+            v[k] = q[j < nv ? j : i];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= v[k].x ^ v[k].w;
+    }
+    return acc;
 }
 
 template <bool LDSIDX>
 __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable tab0,
                                                            DevScratch sc0,
                                                            const int32_t* __restrict__ rows,
-                                                           int32_t nRows) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+                                                           int32_t nRows, int32_t hc) {
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
     const int n = g.n;
     const int lane = threadIdx.x;
     const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
-    int32_t* index2 = LDSIDX ? reinterpret_cast<int32_t*>(smem) : sc.index2 + slot;
+    XEnt* heapGlb = sc.heapEnt + (size_t)blockIdx.x * (size_t)sc.heapStride;
     double* D = sc.dist + slot;
     int32_t* H = sc.hops + slot;
     double* R = sc.rel + slot;
     int32_t* P = sc.pred + slot;
+    // heap and index2 wholly in LDS: one wave, in-order LDS -> no fences
+    const bool fence = !LDSIDX || hc < n;
+    {
+        const size_t m = (size_t)g.rowPtr[n];
+        uint32_t acc = warm_cache(g.rowPtr, (size_t)4 * (n + 1), lane, EX_THREADS);
+        acc ^= warm_cache(g.col, 4 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.lat, 8 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.rel, 8 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.outToIn, 4 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.isAttached, (size_t)n, lane, EX_THREADS);
+        if (acc == 0x5bd1e995u) D[lane] = 0.0;   // keeps the loads; D is rewritten before use
+    }
 
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
         const int r = rows[b];
         const int s = g.attached[r];
-        for (int v = lane; v < n; v += EX_THREADS) index2[v] = 0;
+        XHeap<LDSIDX> h{heapGlb, sc.index2 + slot, hc, 0};
+        for (int v = lane; v < n; v += EX_THREADS) h.set_idx2(v, 0);
         __syncthreads();
-        XHeap h{sc.heapKey + slot, sc.heapIdx + slot, index2, 0};
         if (lane == 0) {
-            xh_push(h, s, 0.0);
+            h.size = 1;
+            h.place(0, XEnt{0.0, 1.0, s, 0});
             H[s] = 0;
             R[s] = 1.0;
             P[s] = -1;
         }
+        __syncthreads();
         int toReach = g.T;
         int hsize = 1;
         while (hsize > 0 && toReach > 0) {
-            int u = 0;
-            double mind = 0.0;
+            // pop (igraph_2wheap_delete_max): the top is known before the
+            // sift-down, so its arc range and attached flag load meanwhile
+            int u = 0, hu = 0;
+            double mind = 0.0, ru = 0.0;
             if (lane == 0) {
-                u = h.idx[0];
-                const double k = h.key[0];
-                xh_switch(h, 0, h.size - 1);
-                h.size -= 1;
-                h.index2[u] = 1;
-                xh_sink(h, 0);
-                mind = -k;
+                const XEnt top = reinterpret_cast<const XEnt*>(ex_smem)[0];   // hc >= 1
+                u = top.idx;
+                mind = -top.key;
+                hu = top.hops;
+                ru = top.rel;
+            }
+            u = __builtin_amdgcn_readfirstlane(u);
+            const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
+            const int att = g.isAttached[u];
+            if (lane == 0) {
+                const int last = h.size - 1;
+                h.size = last;
+                if (last > 0) {
+                    const XEnt e = h.load(last);
+                    h.place(h.sink_hole(0, e.key), e);
+                }
+                h.set_idx2(u, 1);
                 D[u] = mind;
             }
-            u = __shfl(u, 0, 64);
             mind = __shfl(mind, 0, 64);
-            if (g.isAttached[u]) --toReach;
-            const int hu = H[u];
-            const double ru = R[u];
-            const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
+            hu = __shfl(hu, 0, 64);
+            ru = __shfl(ru, 0, 64);
+            if (att) --toReach;
             for (int base = a0; base < a1; base += 64) {
                 const int a = base + lane;
-                int myV = -1, myIn = -1;
-                double myW = 0.0, myR = 0.0;
-                if (a < a1) { myV = g.col[a]; myW = g.lat[a]; myR = g.rel[a]; myIn = g.outToIn[a]; }
-                const int cnt = min(64, a1 - base);
-                for (int k = 0; k < cnt; ++k) {
-                    const int v = __shfl(myV, k, 64);
-                    const double w = __shfl(myW, k, 64);
-                    const double rw = __shfl(myR, k, 64);
-                    const int ia = __shfl(myIn, k, 64);
+                const bool valid = a < a1;
+                const int ac = valid ? a : a0;
+                const int v = g.col[ac];
+                const double w = g.lat[ac];
+                const double rw = g.rel[ac];
+                const int ia = g.outToIn[ac];
+                if (fence) __syncthreads();   // lane 0's global heap/index2 stores visible
+                const int st = valid ? h.idx2(v) : 1;
+                const double alt = mind + w;
+                int need = 0;
+                if (st == 0) need = 1;
+                else if (st >= 2) need = (alt < -h.key(st - 2)) ? 2 : 0;
+                const int nh = hu + 1;
+                const double nr = ru * rw;
+                if (need) { P[v] = ia; H[v] = nh; R[v] = nr; }
+                unsigned long long mask = __ballot(need != 0);
+                while (mask) {
+                    const int k = __builtin_ctzll(mask);
+                    mask &= mask - 1;
+                    const int vk = __builtin_amdgcn_readlane(v, k);
+                    const int nk = __builtin_amdgcn_readlane(need, k);
+                    const int hk = __builtin_amdgcn_readlane(nh, k);
+                    const double ak = __shfl(alt, k, 64);
+                    const double rk = __shfl(nr, k, 64);
                     if (lane == 0) {
-                        const double alt = mind + w;
-                        const int st = h.index2[v];
-                        if (st == 0) {
-                            xh_push(h, v, -alt);
-                            P[v] = ia; H[v] = hu + 1; R[v] = ru * rw;
-                        } else if (st >= 2) {
-                            const double cur = -h.key[st - 2];
-                            if (alt < cur) {
-                                xh_modify(h, v, -alt);
-                                P[v] = ia; H[v] = hu + 1; R[v] = ru * rw;
-                            }
+                        const XEnt e{-ak, rk, vk, hk};
+                        if (nk == 1) {            // igraph_2wheap_push_with_index
+                            const int elem = h.size;
+                            h.size = elem + 1;
+                            h.shift_up_place(elem, e);
+                        } else {                  // igraph_2wheap_modify: sink, then shift_up
+                            const int pos = h.idx2(vk) - 2;
+                            h.shift_up_place(h.sink_hole(pos, e.key), e);
                         }
                     }
                 }
             }
             hsize = __shfl(h.size, 0, 64);
+            if (fence) __syncthreads();
         }
         __syncthreads();
         write_row(g, tab, r, s,
-                  [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
+                  [&](int t) { return h.idx2(t) == 1 ? d2b(D[t]) : INF_BITS; },
                   [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
         __syncthreads();
     }
@@ -1100,20 +1195,22 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
 }
 
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
-                       const int32_t* dRows, int32_t nRows, int32_t grid, bool ldsIndex,
-                       void* stream) {
+                       const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
+                       bool ldsIndex, void* stream) {
     if (nRows <= 0) return;
     if (grid > nRows) grid = nRows;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int bytes = (int)(((size_t)24 * hc + (ldsIndex ? (size_t)4 * g.n : 0) + 15) & ~(size_t)15);
     if (ldsIndex) {
-        const int bytes = (int)(((size_t)4 * g.n + 15) & ~(size_t)15);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         hipLaunchKernelGGL(k_exact_rows<true>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab,
-                           sc, dRows, nRows);
+                           sc, dRows, nRows, hc);
     } else {
-        hipLaunchKernelGGL(k_exact_rows<false>, dim3(grid), dim3(EX_THREADS), 0, st, g, tab, sc,
-                           dRows, nRows);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipLaunchKernelGGL(k_exact_rows<false>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab,
+                           sc, dRows, nRows, hc);
     }
 }
 

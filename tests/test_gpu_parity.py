@@ -99,6 +99,23 @@ def test_forced_exact_kernel_all_rows(E, oracle_mod):
     assert st["rowsExact"] == 300
 
 
+def test_exact_kernel_heap_tail_in_global(E, oracle_mod, monkeypatch):
+    """k_exact_rows with only 5 heap entries in LDS: the rest of the igraph
+    2-way heap lives in the global slot (the split the large graphs use)."""
+    monkeypatch.setenv("SHDPE_EXACT_HC", "5")
+    top = G.random_sparse(300, 5, seed=11, quantum=2.0)
+    st = _check_engine(E, oracle_mod, top, np.arange(0, 300, 3), force=3)
+    assert st["rowsExact"] == 100
+
+
+def test_exact_kernel_large_graph_global_index(E, oracle_mod):
+    """n > 24k: index2 in global memory, heap head in LDS, tail in global."""
+    top = G.power_law(30_000, m=2, seed=12)
+    att = G.sample_attached(top.n, 600, seed=4)
+    st = _check_engine(E, oracle_mod, top, att, sources=att[:6], force=3)
+    assert st["rowsExact"] == 6
+
+
 def test_shipped_minus_one_edge_ties(E, oracle_mod):
     top = Topology.load_npz(os.path.join(GOLDEN, "shipped_topology.npz"))
     m1 = G.minus_one_edge(top, seed=3)
