@@ -58,25 +58,28 @@ struct alignas(16) BCtrl {
 // Forward reliability fold with vertex factors (topology.c:1430-1462, :1499)
 // along lane l's predecessor chain, multiplied in source -> target order.
 template <int LB>
-__device__ __noinline__ double fold_rel_batch(const DevGraph& g, const int32_t* P, int l, int s,
-                                              int t, int h) {
-    double acc = 1.0 * g.vrel[s];
-    acc = acc * g.vrel[t];
+__device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
+                                              const double* __restrict__ inRel,
+                                              const int32_t* __restrict__ inCol,
+                                              const int32_t* P, int l, int s, int t, int h) {
+    // (arrays by value: a DevGraph& would pin the caller's descriptor in scratch)
+    double acc = 1.0 * vrel[s];
+    acc = acc * vrel[t];
     if (h <= 64) {
         double fac[64];
         int k = 0, x = t;
         while (x != s && k < 64) {
             const int a = ld_wg(&P[(size_t)x * LB + l]);
-            fac[k++] = g.inRel[a];
-            x = g.inCol[a];
+            fac[k++] = inRel[a];
+            x = inCol[a];
         }
         for (int i = k - 1; i >= 0; --i) acc = acc * fac[i];
         return acc;
     }
     for (int d = 1; d <= h; ++d) {
         int x = t;
-        for (int up = 0; up < h - d; ++up) x = g.inCol[ld_wg(&P[(size_t)x * LB + l])];
-        acc = acc * g.inRel[ld_wg(&P[(size_t)x * LB + l])];
+        for (int up = 0; up < h - d; ++up) x = inCol[ld_wg(&P[(size_t)x * LB + l])];
+        acc = acc * inRel[ld_wg(&P[(size_t)x * LB + l])];
     }
     return acc;
 }
@@ -619,7 +622,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                         if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
                             Rl = ld_wg(&R[e]);
                         else
-                            Rl = fold_rel_batch<LB>(g, P, l, src, t, h);
+                            Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
                         if (L == 0.0) {                 // topology.c:1848-1852
                             L = 1.0;
                             f |= F_ZEROLAT;

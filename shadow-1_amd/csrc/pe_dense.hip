@@ -11,14 +11,13 @@
 // distinct minima -> tie row, resolved by k_exact_rows on the CSR).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "pe_device.hpp"
 
 namespace shdpe {
 
 constexpr double DINF = __builtin_huge_val();
-constexpr int TS = 64;      // output tile (sources x targets)
-constexpr int KC = 32;      // K chunk staged in LDS
-constexpr int MT = 4;       // micro-tile per thread (MT x MT)
 
 template <class T>
 __device__ __forceinline__ T* dglobal(T* p) {
@@ -58,156 +57,183 @@ __global__ __launch_bounds__(256) void k_dense_init(DevGraph g, const double* W,
     if (v == 0) dglobal(rowActive)[b] = 1;
 }
 
-// One in-place min-plus sweep over all active row tiles.  Tile = 64 sources
-// x 64 targets; 256 threads, 4x4 micro-tile each; K chunks of 32 staged in
-// LDS (A transposed).  rowActive: row improved in the previous sweep (a row
-// that did not change cannot change again: its update only reads itself).
-__global__ __launch_bounds__(256) void k_minplus_sweep(const double* W, double* D, int64_t n,
-                                                       int64_t ldD, int32_t nRows,
-                                                       const uint8_t* rowActive,
-                                                       uint8_t* rowChanged, int32_t* anyChanged) {
-    __shared__ double At[KC][TS + 2];
-    __shared__ double Bs[KC][TS + 2];
+// Min-plus tiles.  A workgroup (256 threads = 16 x 16) owns 16*MI source
+// rows x 128 targets; thread (tx, ty) holds rows ty + 16 i (i < MI) and
+// targets tx + 16 j (j < 8), so LDS reads are broadcast (A) or consecutive
+// doubles (B) and the D / P stores of a wave are 128-B runs.  K is streamed
+// in chunks of 16: D[rows][k0..k0+16) (staged transposed) and
+// W[k0..k0+16)[targets] are prefetched into registers while the previous
+// chunk is consumed from LDS.
+//   SWEEP: acc = min(acc, a + b) -> in-place D update (chaotic Bellman-Ford
+//          on rows; every relaxation is dist[u] + w, Appendix B);
+//   PRED:  among u with fl(D[s][u] + W[u][v]) == D[s][v] keep the minimum
+//          D[s][u] (igraph's first-popped tight predecessor) and its u; a
+//          second u at the same minimum, or a zero-increment u, marks the
+//          row tie-ambiguous (-> k_exact_rows).  A tight u is rare (about
+//          one of n per entry), so the per-chunk test is add + compare and
+//          the bookkeeping runs only when some lane of the wave hits.
+constexpr int MJ = 8;          // targets per thread
+constexpr int TCOL = 16 * MJ;  // 128 targets per tile
+constexpr int KB = 16;         // K chunk
+enum { MP_SWEEP = 0, MP_PRED = 1 };
+
+template <int MODE, int MI>
+__global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, double* D, int64_t n,
+                                                 int64_t ldD, int32_t nRows,
+                                                 const uint8_t* rowActive, uint8_t* rowChanged,
+                                                 int32_t* anyChanged, const int32_t* rows,
+                                                 int32_t* P, uint8_t* rowAmb) {
+    constexpr int TR = 16 * MI;
+    __shared__ double At[KB][TR + 1];
+    __shared__ double Bs[KB][TCOL];
     __shared__ int tileActive;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int64_t v0 = (int64_t)blockIdx.x * TS;
-    const int r0 = blockIdx.y * TS;
+    const int tid = threadIdx.x;
+    const int tx = tid & 15, ty = tid >> 4;
+    const int64_t v0 = (int64_t)blockIdx.x * TCOL;
+    const int r0 = blockIdx.y * TR;
     const double* __restrict__ Wg = dglobal(W);
     double* Dg = dglobal(D);
-    if (threadIdx.x == 0) tileActive = 0;
-    __syncthreads();
-    if (threadIdx.x < TS && r0 + threadIdx.x < nRows && dglobal(rowActive)[r0 + threadIdx.x])
-        tileActive = 1;
-    __syncthreads();
-    if (!tileActive) return;
+    if (MODE == MP_SWEEP) {
+        if (tid == 0) tileActive = 0;
+        __syncthreads();
+        if (tid < TR && r0 + tid < nRows && dglobal(rowActive)[r0 + tid]) tileActive = 1;
+        __syncthreads();
+        if (!tileActive) return;
+    }
 
-    double acc[MT][MT];
+    // staging coordinates (fixed per thread); one base pointer per operand,
+    // per-chunk offsets are uniform -> few live address registers
+    const int aK = tid & 15, aR = tid >> 4;          // A: row aR + 16 q, column k0 + aK
+    const int bK = tid >> 7, bC = tid & 127;         // B: row k0 + bK + 2 q, column v0 + bC
+    const bool bColOk = v0 + bC < n;
+    const double* pA = Dg + (int64_t)(r0 + aR) * ldD + aK;
+    const double* pB = Wg + (int64_t)bK * n + v0 + bC;
+    int rmask = 0;
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int q = 0; q < MI; ++q) rmask |= (r0 + aR + 16 * q < nRows) << q;
+    double ra[MI], rb[KB / 2];
+    auto fetch = [&](int64_t k0) {
+        const bool uok = k0 + aK < n;
 #pragma unroll
-        for (int j = 0; j < MT; ++j) acc[i][j] = DINF;
+        for (int q = 0; q < MI; ++q) {
+            const bool ok = uok && ((rmask >> q) & 1);
+            const double x = pA[ok ? (int64_t)q * 16 * ldD + k0 : 0];
+            ra[q] = ok ? x : DINF;
+        }
+#pragma unroll
+        for (int q = 0; q < KB / 2; ++q) {
+            const int64_t u = k0 + bK + 2 * q;
+            const bool ok = u < n && bColOk;
+            const double x = pB[ok ? (k0 + 2 * q) * n : 0];
+            rb[q] = ok ? x : DINF;
+        }
+    };
 
-    for (int64_t k0 = 0; k0 < n; k0 += KC) {
-        // stage A (D rows r0.., cols k0..) transposed and B (W rows k0.., cols v0..)
-        for (int e = threadIdx.x; e < TS * KC; e += 256) {
-            const int rr = e / KC, kk = e % KC;
-            const int64_t u = k0 + kk;
-            At[kk][rr] = (r0 + rr < nRows && u < n) ? Dg[(int64_t)(r0 + rr) * ldD + u] : DINF;
-            const int kb = e / TS, cc = e % TS;
-            const int64_t ub = k0 + kb, vb = v0 + cc;
-            Bs[kb][cc] = (ub < n && vb < n) ? Wg[ub * n + vb] : DINF;
-        }
-        __syncthreads();
-#pragma unroll 8
-        for (int kk = 0; kk < KC; ++kk) {
-            double a[MT], b[MT];
+    double acc[MI][MJ];     // SWEEP: running min; PRED: target distance
+    double best[MODE == MP_PRED ? MI : 1][MJ];
+    int arg[MODE == MP_PRED ? MI : 1][MJ];   // -1 none, >= 0 unique, -2 tie
 #pragma unroll
-            for (int i = 0; i < MT; ++i) a[i] = At[kk][ty * MT + i];
+    for (int i = 0; i < MI; ++i) {
+        const int r = r0 + ty + 16 * i;
 #pragma unroll
-            for (int j = 0; j < MT; ++j) b[j] = Bs[kk][tx * MT + j];
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = 0; j < MT; ++j) acc[i][j] = fmin(acc[i][j], a[i] + b[j]);
-        }
-        __syncthreads();
-    }
-    int changed = 0;
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int r = r0 + ty * MT + i;
-        if (r >= nRows) continue;
-        int rowCh = 0;
-#pragma unroll
-        for (int j = 0; j < MT; ++j) {
-            const int64_t v = v0 + tx * MT + j;
-            if (v >= n) continue;
-            double* p = Dg + (int64_t)r * ldD + v;
-            if (acc[i][j] < *p) { *p = acc[i][j]; rowCh = 1; }
-        }
-        if (rowCh) { dglobal(rowChanged)[r] = 1; changed = 1; }
-    }
-    if (changed) atomicOr(dglobal(anyChanged), 1);
-}
-
-// Predecessor pass: for every (source row, target v): among u with
-// fl(D[s][u] + W[u][v]) == D[s][v] take the minimum D[s][u]; a second u with
-// the same minimum (or a zero-increment u) makes the row tie-ambiguous.
-__global__ __launch_bounds__(256) void k_minplus_pred(DevGraph g, const double* W, const double* D,
-                                                      int64_t n, int64_t ldD, int32_t nRows,
-                                                      const int32_t* rows, int32_t* P,
-                                                      uint8_t* rowAmb) {
-    __shared__ double At[KC][TS + 2];
-    __shared__ double Bs[KC][TS + 2];
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int64_t v0 = (int64_t)blockIdx.x * TS;
-    const int r0 = blockIdx.y * TS;
-    const double* __restrict__ Wg = dglobal(W);
-    const double* Dg = dglobal(D);
-    double tgt[MT][MT], best[MT][MT];
-    int arg[MT][MT], cnt[MT][MT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int r = r0 + ty * MT + i;
-#pragma unroll
-        for (int j = 0; j < MT; ++j) {
-            const int64_t v = v0 + tx * MT + j;
-            tgt[i][j] = (r < nRows && v < n) ? Dg[(int64_t)r * ldD + v] : -1.0;
-            best[i][j] = DINF;
-            arg[i][j] = -1;
-            cnt[i][j] = 0;
-        }
-    }
-    for (int64_t k0 = 0; k0 < n; k0 += KC) {
-        for (int e = threadIdx.x; e < TS * KC; e += 256) {
-            const int rr = e / KC, kk = e % KC;
-            const int64_t u = k0 + kk;
-            At[kk][rr] = (r0 + rr < nRows && u < n) ? Dg[(int64_t)(r0 + rr) * ldD + u] : DINF;
-            const int kb = e / TS, cc = e % TS;
-            const int64_t ub = k0 + kb, vb = v0 + cc;
-            Bs[kb][cc] = (ub < n && vb < n) ? Wg[ub * n + vb] : DINF;
-        }
-        __syncthreads();
-        for (int kk = 0; kk < KC; ++kk) {
-            double a[MT], b[MT];
-#pragma unroll
-            for (int i = 0; i < MT; ++i) a[i] = At[kk][ty * MT + i];
-#pragma unroll
-            for (int j = 0; j < MT; ++j) b[j] = Bs[kk][tx * MT + j];
-            const int u = (int)(k0 + kk);
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = 0; j < MT; ++j) {
-                    if (a[i] + b[j] == tgt[i][j]) {
-                        if (a[i] < best[i][j]) { best[i][j] = a[i]; arg[i][j] = u; cnt[i][j] = 1; }
-                        else if (a[i] == best[i][j]) ++cnt[i][j];
-                    }
-                }
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const int r = r0 + ty * MT + i;
-        if (r >= nRows) continue;
-        const int src = dglobal(g.attached)[dglobal(rows)[r]];
-        int amb = 0;
-#pragma unroll
-        for (int j = 0; j < MT; ++j) {
-            const int64_t v = v0 + tx * MT + j;
-            if (v >= n) continue;
-            int p = -1;
-            if (v != src && tgt[i][j] < DINF) {
-                p = arg[i][j];
-                // cnt != 1: two minima, or (tgt == best) a zero-increment arc
-                if (cnt[i][j] != 1 || best[i][j] == tgt[i][j]) amb = 1;
+        for (int j = 0; j < MJ; ++j) {
+            if (MODE == MP_SWEEP) {
+                acc[i][j] = DINF;
+            } else {
+                const int64_t v = v0 + tx + 16 * j;
+                acc[i][j] = (r < nRows && v < n) ? Dg[(int64_t)r * ldD + v] : -1.0;
+                best[i][j] = DINF;
+                arg[i][j] = -1;
             }
-            dglobal(P)[(int64_t)r * ldD + v] = p;
         }
-        if (amb) dglobal(rowAmb)[r] = 1;
+    }
+
+    fetch(0);
+    for (int64_t k0 = 0; k0 < n; k0 += KB) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < MI; ++q) At[aK][aR + 16 * q] = ra[q];
+#pragma unroll
+        for (int q = 0; q < KB / 2; ++q) Bs[bK + 2 * q][bC] = rb[q];
+        __syncthreads();
+        if (k0 + KB < n) fetch(k0 + KB);
+#pragma unroll 4
+        for (int kk = 0; kk < KB; ++kk) {
+            double a[MI], b[MJ];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) a[i] = At[kk][ty + 16 * i];
+#pragma unroll
+            for (int j = 0; j < MJ; ++j) b[j] = Bs[kk][tx + 16 * j];
+            if (MODE == MP_SWEEP) {
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < MJ; ++j) acc[i][j] = fmin(acc[i][j], a[i] + b[j]);
+            } else {
+                bool hit = false;
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < MJ; ++j) hit |= (a[i] + b[j] == acc[i][j]);
+                if (__any(hit)) {
+                    const int u = (int)(k0 + kk);
+#pragma unroll
+                    for (int i = 0; i < MI; ++i)
+#pragma unroll
+                        for (int j = 0; j < MJ; ++j) {
+                            if (a[i] + b[j] == acc[i][j]) {
+                                if (a[i] < best[i][j]) { best[i][j] = a[i]; arg[i][j] = u; }
+                                else if (a[i] == best[i][j]) arg[i][j] = -2;
+                            }
+                        }
+                }
+            }
+        }
+    }
+
+    if (MODE == MP_SWEEP) {
+        int changed = 0;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int r = r0 + ty + 16 * i;
+            if (r >= nRows) continue;
+            int rowCh = 0;
+#pragma unroll
+            for (int j = 0; j < MJ; ++j) {
+                const int64_t v = v0 + tx + 16 * j;
+                if (v >= n) continue;
+                double* p = Dg + (int64_t)r * ldD + v;
+                if (acc[i][j] < *p) { *p = acc[i][j]; rowCh = 1; }
+            }
+            if (rowCh) { dglobal(rowChanged)[r] = 1; changed = 1; }
+        }
+        if (changed) atomicOr(dglobal(anyChanged), 1);
+    } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int r = r0 + ty + 16 * i;
+            if (r >= nRows) continue;
+            const int src = dglobal(g.attached)[dglobal(rows)[r]];
+            int amb = 0;
+#pragma unroll
+            for (int j = 0; j < MJ; ++j) {
+                const int64_t v = v0 + tx + 16 * j;
+                if (v >= n) continue;
+                int p = -1;
+                if (v != src && acc[i][j] < DINF) {
+                    p = arg[i][j];
+                    // two minima, or (target == best) a zero-increment arc
+                    if (p < 0 || best[i][j] == acc[i][j]) amb = 1;
+                }
+                dglobal(P)[(int64_t)r * ldD + v] = p;
+            }
+            if (amb) dglobal(rowAmb)[r] = 1;
+        }
     }
 }
+
+constexpr int MI_SWEEP = 6;
+constexpr int MI_PRED = 2;
 
 // Row writer: lat = D, hops / rel by walking the (short) predecessor chain
 // and folding rel in source->target order (topology.c:1430-1499).
@@ -288,21 +314,32 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
     hipLaunchKernelGGL(k_dense_init, dim3((unsigned)((n + 255) / 256), nRows), dim3(256), 0, st, g,
                        W, D, dRows, n, ldD, rowActive);
     (void)hipMemsetAsync(rowAmb, 0, nRows, st);
-    const dim3 grid((unsigned)((n + TS - 1) / TS), (unsigned)((nRows + TS - 1) / TS));
+    const unsigned gx = (unsigned)((n + TCOL - 1) / TCOL);
+    const dim3 gridS(gx, (unsigned)((nRows + 16 * MI_SWEEP - 1) / (16 * MI_SWEEP)));
+    static const int predMi = [] {
+        const char* e = std::getenv("SHDPE_PRED_MI");
+        return e && *e ? std::atoi(e) : MI_PRED;
+    }();
+    const int miP = predMi == 2 ? 2 : MI_PRED;
+    const dim3 gridP(gx, (unsigned)((nRows + 16 * miP - 1) / (16 * miP)));
     int sweeps = 0;
     for (;; ++sweeps) {
         (void)hipMemsetAsync(rowChanged, 0, nRows, st);
         (void)hipMemsetAsync(dAny, 0, 4, st);
-        hipLaunchKernelGGL(k_minplus_sweep, grid, dim3(256), 0, st, W, D, n, ldD, nRows, rowActive,
-                           rowChanged, dAny);
+        hipLaunchKernelGGL((k_minplus<MP_SWEEP, MI_SWEEP>), gridS, dim3(256), 0, st, g, W, D, n,
+                           ldD, nRows, rowActive, rowChanged, dAny, dRows, P, rowAmb);
         int any = 0;
         if (hipMemcpyAsync(&any, dAny, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
         if (hipStreamSynchronize(st) != hipSuccess) return -1;
         std::swap(rowActive, rowChanged);
         if (!any || sweeps > n) break;
     }
-    hipLaunchKernelGGL(k_minplus_pred, grid, dim3(256), 0, st, g, W, D, n, ldD, nRows, dRows, P,
-                       rowAmb);
+    if (miP == 2)
+        hipLaunchKernelGGL((k_minplus<MP_PRED, 2>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
+                           rowActive, rowChanged, dAny, dRows, P, rowAmb);
+    else
+        hipLaunchKernelGGL((k_minplus<MP_PRED, MI_PRED>), gridP, dim3(256), 0, st, g, W, D, n, ldD,
+                           nRows, rowActive, rowChanged, dAny, dRows, P, rowAmb);
     hipLaunchKernelGGL(k_dense_write, dim3((unsigned)((g.T + 255) / 256), nRows), dim3(256), 0, st,
                        g, tab, D, P, Rl, n, ldD, dRows, rowAmb);
     if (sweepsOut) *sweepsOut = sweeps + 1;
