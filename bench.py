@@ -153,10 +153,12 @@ def main():
         kname = "k_direct_rows"
         achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     elif st["mode"] == 3:
-        # dense min-plus: FP64 VALU roof, 2*n^2 flops per row per sweep
-        sweeps = st["denseSweeps"] / max(1, st["launchesDense"])
-        bytes_per_launch = 2.0 * n * n * count * (sweeps + 1)       # + predecessor pass
-        kname = "k_minplus_sweep"
+        # dense min-plus: FP64 VALU roof.  SURVEY §8d prices a sweep at 2*n^2
+        # flops per row; sweeps skip K chunks that cannot improve (chunk
+        # epochs), so the work counted is what the kernels executed: visited
+        # (row tile, K chunk) pairs x 2 flops per relaxation, + the pred pass
+        bytes_per_launch = st["denseFlops"] / max(1, st["launchesDense"])
+        kname = "k_minplus"
         bound, unit, peak = "valu-fp64", "TFLOP/s", FP64_VALU_PEAK_TF
         achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e12
     else:

@@ -103,6 +103,8 @@ typedef struct ShdPeStats {
     double msDenseKernel;      /* device time of the dense min-plus path           */
     int64_t launchesDense;
     int64_t denseSweeps;       /* min-plus sweeps (incl. the confirming one)       */
+    double denseFlops;         /* executed min-plus work: 2 per (s,u,v) visited,
+                                  sweeps (skipped K chunks excluded) + pred pass */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */

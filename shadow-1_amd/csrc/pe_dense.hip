@@ -11,7 +11,10 @@
 // distinct minima -> tie row, resolved by k_exact_rows on the CSR).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "pe_device.hpp"
 
@@ -75,6 +78,7 @@ __global__ __launch_bounds__(256) void k_dense_init(DevGraph g, const double* W,
 constexpr int MJ = 8;          // targets per thread
 constexpr int TCOL = 16 * MJ;  // 128 targets per tile
 constexpr int KB = 16;         // K chunk
+constexpr int MAXCH = 4096;    // chunk list capacity (n <= 65536 uses chunk epochs)
 enum { MP_SWEEP = 0, MP_PRED = 1 };
 
 template <int MODE, int MI>
@@ -82,11 +86,14 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
                                                  int64_t ldD, int32_t nRows,
                                                  const uint8_t* rowActive, uint8_t* rowChanged,
                                                  int32_t* anyChanged, const int32_t* rows,
-                                                 int32_t* P, uint8_t* rowAmb) {
+                                                 int32_t* P, uint8_t* rowAmb,
+                                                 uint8_t* chunkEpoch, int32_t epoch) {
     constexpr int TR = 16 * MI;
     __shared__ double At[KB][TR + 1];
     __shared__ double Bs[KB][TCOL];
     __shared__ int tileActive;
+    __shared__ int nAct;
+    __shared__ uint16_t actList[MAXCH];
     const int tid = threadIdx.x;
     const int tx = tid & 15, ty = tid >> 4;
     const int64_t v0 = (int64_t)blockIdx.x * TCOL;
@@ -100,6 +107,28 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
         __syncthreads();
         if (!tileActive) return;
     }
+    // K chunks to visit.  SWEEP with chunk epochs (epoch > 0): only chunks u
+    // of this row tile whose D[s][u] changed in the previous sweep or in this
+    // one (a D[s][u] unchanged since this tile last read it cannot improve
+    // D[s][v] again); the visiting order is irrelevant (min is exact and
+    // order-free).  Otherwise every chunk, in order.
+    const int nch = (int)((n + KB - 1) / KB);
+    const bool useList = MODE == MP_SWEEP && epoch > 0;
+    if (useList) {
+        if (tid == 0) nAct = 0;
+        __syncthreads();
+        const uint8_t* ce = dglobal(chunkEpoch) + (size_t)blockIdx.y * nch;
+        for (int c = tid; c < nch; c += 256)
+            if ((int)ce[c] >= epoch - 1) actList[atomicAdd(&nAct, 1)] = (uint16_t)c;
+        __syncthreads();
+    }
+    const int nVisit = useList ? nAct : nch;
+    if (nVisit == 0) return;
+    // work accounting: visited (row tile, K chunk) pairs (anyChanged[2..3] = u64)
+    if (MODE == MP_SWEEP && tid == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(dglobal(anyChanged) + 2),
+                  (unsigned long long)nVisit);
+    auto chunkK = [&](int c) -> int64_t { return (int64_t)(useList ? (int)actList[c] : c) * KB; };
 
     // staging coordinates (fixed per thread); one base pointer per operand,
     // per-chunk offsets are uniform -> few live address registers
@@ -148,15 +177,16 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
         }
     }
 
-    fetch(0);
-    for (int64_t k0 = 0; k0 < n; k0 += KB) {
+    fetch(chunkK(0));
+    for (int c = 0; c < nVisit; ++c) {
+        const int64_t k0 = chunkK(c);
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < MI; ++q) At[aK][aR + 16 * q] = ra[q];
 #pragma unroll
         for (int q = 0; q < KB / 2; ++q) Bs[bK + 2 * q][bC] = rb[q];
         __syncthreads();
-        if (k0 + KB < n) fetch(k0 + KB);
+        if (c + 1 < nVisit) fetch(chunkK(c + 1));
 #pragma unroll 4
         for (int kk = 0; kk < KB; ++kk) {
             double a[MI], b[MJ];
@@ -193,6 +223,7 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
 
     if (MODE == MP_SWEEP) {
         int changed = 0;
+        int colCh = 0;      // bit j: some row of mine changed in chunk v0/16 + j
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             const int r = r0 + ty + 16 * i;
@@ -203,11 +234,18 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
                 const int64_t v = v0 + tx + 16 * j;
                 if (v >= n) continue;
                 double* p = Dg + (int64_t)r * ldD + v;
-                if (acc[i][j] < *p) { *p = acc[i][j]; rowCh = 1; }
+                if (acc[i][j] < *p) { *p = acc[i][j]; ++rowCh; colCh |= 1 << j; }
             }
-            if (rowCh) { dglobal(rowChanged)[r] = 1; changed = 1; }
+            if (rowCh) { dglobal(rowChanged)[r] = 1; changed += rowCh; }
         }
-        if (changed) atomicOr(dglobal(anyChanged), 1);
+        if (epoch > 0 && colCh) {
+            uint8_t* ce = dglobal(chunkEpoch) + (size_t)blockIdx.y * nch + (v0 / KB);
+#pragma unroll
+            for (int j = 0; j < MJ; ++j)
+                if ((colCh >> j) & 1) ce[j] = (uint8_t)epoch;
+        }
+        // anyChanged counts improved entries (debug statistics; > 0 = not converged)
+        if (changed) atomicAdd(dglobal(anyChanged), changed);
     } else {
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
@@ -307,8 +345,9 @@ void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int
 
 int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, const double* Rl,
                       double* D, int32_t* P, uint8_t* rowActive, uint8_t* rowChanged,
-                      uint8_t* rowAmb, int32_t* dAny, const int32_t* dRows, int32_t nRows,
-                      int64_t n, void* stream, int* sweepsOut) {
+                      uint8_t* rowAmb, int32_t* dAny, uint8_t* chunkEpoch, const int32_t* dRows,
+                      int32_t nRows, int64_t n, void* stream, int* sweepsOut,
+                      double* flopsOut) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t ldD = n;
     hipLaunchKernelGGL(k_dense_init, dim3((unsigned)((n + 255) / 256), nRows), dim3(256), 0, st, g,
@@ -322,27 +361,53 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
     }();
     const int miP = predMi == 2 ? 2 : MI_PRED;
     const dim3 gridP(gx, (unsigned)((nRows + 16 * miP - 1) / (16 * miP)));
+    // chunk epochs (uint8): sweep t visits chunks changed at t-1 or t; the
+    // initial rows count as changed at epoch 0.  Off beyond 250 sweeps or
+    // when the chunk list would not fit.
+    const int64_t nch = (n + KB - 1) / KB;
+    const bool epochs = nch <= MAXCH && !std::getenv("SHDPE_DENSE_NO_EPOCH");
+    if (epochs)
+        (void)hipMemsetAsync(chunkEpoch, 0, (size_t)gridS.y * (size_t)nch, st);
     int sweeps = 0;
+    double visits = 0.0;
     for (;; ++sweeps) {
         (void)hipMemsetAsync(rowChanged, 0, nRows, st);
-        (void)hipMemsetAsync(dAny, 0, 4, st);
+        (void)hipMemsetAsync(dAny, 0, 16, st);
+        const int epoch = (epochs && sweeps + 1 < 250) ? sweeps + 1 : 0;
         hipLaunchKernelGGL((k_minplus<MP_SWEEP, MI_SWEEP>), gridS, dim3(256), 0, st, g, W, D, n,
-                           ldD, nRows, rowActive, rowChanged, dAny, dRows, P, rowAmb);
-        int any = 0;
-        if (hipMemcpyAsync(&any, dAny, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
+                           ldD, nRows, rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch,
+                           epoch);
+        int32_t cnt[4] = {0, 0, 0, 0};
+        if (hipMemcpyAsync(cnt, dAny, 16, hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
         if (hipStreamSynchronize(st) != hipSuccess) return -1;
+        const int any = cnt[0];
+        unsigned long long vis = 0;
+        std::memcpy(&vis, &cnt[2], 8);
+        visits += (double)vis;
         std::swap(rowActive, rowChanged);
+        if (std::getenv("SHDPE_DEBUG")) {
+            std::vector<uint8_t> h(nRows);
+            (void)hipMemcpy(h.data(), rowActive, nRows, hipMemcpyDeviceToHost);
+            long c = 0;
+            for (uint8_t x : h) c += x;
+            std::fprintf(stderr, "[shdpe] dense sweep %d: rows changed %ld of %d, entries %d\n", sweeps,
+                         c, nRows, any);
+        }
         if (!any || sweeps > n) break;
     }
     if (miP == 2)
         hipLaunchKernelGGL((k_minplus<MP_PRED, 2>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
-                           rowActive, rowChanged, dAny, dRows, P, rowAmb);
+                           rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
     else
         hipLaunchKernelGGL((k_minplus<MP_PRED, MI_PRED>), gridP, dim3(256), 0, st, g, W, D, n, ldD,
-                           nRows, rowActive, rowChanged, dAny, dRows, P, rowAmb);
+                           nRows, rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
     hipLaunchKernelGGL(k_dense_write, dim3((unsigned)((g.T + 255) / 256), nRows), dim3(256), 0, st,
                        g, tab, D, P, Rl, n, ldD, dRows, rowAmb);
     if (sweepsOut) *sweepsOut = sweeps + 1;
+    // flops: 2 per relaxation; a visit = TR rows x 128 targets x KB u (tile
+    // nominal size); the pred pass is one full n x n pass per row
+    if (flopsOut)
+        *flopsOut = 2.0 * visits * (16.0 * MI_SWEEP) * TCOL * KB + 2.0 * (double)n * n * nRows;
     return 0;
 }
 

@@ -141,7 +141,8 @@ void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int
                         void* stream);
 int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, const double* Rl,
                       double* D, int32_t* P, uint8_t* rowActive, uint8_t* rowChanged,
-                      uint8_t* rowAmb, int32_t* dAny, const int32_t* dRows, int32_t nRows,
-                      int64_t n, void* stream, int* sweepsOut);
+                      uint8_t* rowAmb, int32_t* dAny, uint8_t* chunkEpoch, const int32_t* dRows,
+                      int32_t nRows, int64_t n, void* stream, int* sweepsOut,
+                      double* flopsOut);
 
 }  // namespace shdpe

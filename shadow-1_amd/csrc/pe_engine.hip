@@ -61,6 +61,7 @@ struct ShdPe {
     uint8_t* dRowA = nullptr;
     uint8_t* dRowB = nullptr;
     uint8_t* dRowAmbD = nullptr;
+    uint8_t* dChunkEpoch = nullptr;   // dense: last sweep that changed (row tile, K chunk)
     int32_t* dAny = nullptr;
     int32_t denseRows = 0;
     ShdPeStats stats{};
@@ -450,7 +451,7 @@ static int ensure_dense(ShdPe* pe) {
     const int64_t n = pe->hg.n;
     const int64_t T = (int64_t)pe->attached.size();
     int rc;
-    void *w, *rl, *d, *p, *ra, *rb, *am, *any;
+    void *w, *rl, *d, *p, *ra, *rb, *am, *any, *ce;
     // rows per batch: D (f64) + P (i32) per row
     const int64_t budget = (int64_t)env_double("SHDPE_DENSE_BATCH_GB", 24.0) * (1LL << 30);
     int64_t rows = std::max<int64_t>(64, budget / (n * 12));
@@ -458,8 +459,10 @@ static int ensure_dense(ShdPe* pe) {
     if ((rc = dev_alloc(pe, &w, (size_t)(n * n * 8))) || (rc = dev_alloc(pe, &rl, (size_t)(n * n * 8))) ||
         (rc = dev_alloc(pe, &d, (size_t)(rows * n * 8))) || (rc = dev_alloc(pe, &p, (size_t)(rows * n * 4))) ||
         (rc = dev_alloc(pe, &ra, (size_t)rows)) || (rc = dev_alloc(pe, &rb, (size_t)rows)) ||
-        (rc = dev_alloc(pe, &am, (size_t)rows)) || (rc = dev_alloc(pe, &any, 16)))
+        (rc = dev_alloc(pe, &am, (size_t)rows)) || (rc = dev_alloc(pe, &any, 16)) ||
+        (rc = dev_alloc(pe, &ce, (size_t)((rows / 16 + 1) * (n / 16 + 1)))))
         return rc;
+    pe->dChunkEpoch = (uint8_t*)ce;
     pe->dW = (double*)w; pe->dRl = (double*)rl; pe->dD = (double*)d; pe->dP = (int32_t*)p;
     pe->dRowA = (uint8_t*)ra; pe->dRowB = (uint8_t*)rb; pe->dRowAmbD = (uint8_t*)am;
     pe->dAny = (int32_t*)any;
@@ -506,9 +509,11 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
                 const int32_t dc = std::min(pe->denseRows, cnt - d0);
                 HIPCHK(hipEventRecord(pe->evA, pe->stream));
                 int sweeps = 0;
+                double flops = 0.0;
                 if (launch_dense_rows(pe->dg, pe->tab, pe->dW, pe->dRl, pe->dD, pe->dP, pe->dRowA,
-                                      pe->dRowB, pe->dRowAmbD, pe->dAny, pe->dRows + d0, dc,
-                                      pe->hg.n, pe->stream, &sweeps))
+                                      pe->dRowB, pe->dRowAmbD, pe->dAny, pe->dChunkEpoch,
+                                      pe->dRows + d0, dc,
+                                      pe->hg.n, pe->stream, &sweeps, &flops))
                     return SHD_PE_EHIP;
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(pe->evB, pe->stream));
@@ -519,6 +524,7 @@ static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count
                 pe->stats.msDenseKernel += elapsed(pe->evA, pe->evB);
                 pe->stats.launchesDense++;
                 pe->stats.denseSweeps += sweeps;
+                pe->stats.denseFlops += flops;
                 for (int32_t i = 0; i < dc; ++i)
                     if (amb[i]) exactRows.push_back(pos[c0 + d0 + i]);
             }

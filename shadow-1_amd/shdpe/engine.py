@@ -53,7 +53,7 @@ class Stats(C.Structure):
                 ("mode", C.c_int32), ("isComplete", C.c_int32), ("nVertices", C.c_int32),
                 ("nArcs", C.c_int64), ("nAttached", C.c_int32), ("deltaUsed", C.c_double),
                 ("msDenseKernel", C.c_double), ("launchesDense", C.c_int64),
-                ("denseSweeps", C.c_int64)]
+                ("denseSweeps", C.c_int64), ("denseFlops", C.c_double)]
 
 
 class EngineError(RuntimeError):
