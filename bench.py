@@ -80,6 +80,9 @@ def main():
     ap.add_argument("--allgather", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--d2h-rows", type=int, default=2048,
+                    help="rows copied to host buffers through shd_pe_get_row after the timed "
+                         "region (PCIe-inclusive rate, reported separately; 0 = off)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,6 +145,20 @@ def main():
         gather = {"bytes_per_rank": mine.numel() * 8, "ms": (g1 - g0) * 1e3,
                   "field": "latency f64"}
 
+    d2h = None
+    if args.d2h_rows > 0 and count > 0:
+        # PCIe-inclusive: the shard's rows into host buffers (shd_pe_get_rows,
+        # pinned double-buffered staging), after the timed region
+        k = min(args.d2h_rows, count)
+        eng.get_rows(start, min(k, 8))
+        d0 = time.perf_counter()
+        eng.get_rows(start, k)
+        dt = time.perf_counter() - d0
+        row_bytes = T * (8 + 8 + 4 + 1 + (4 if eng.store_pred else 0))
+        d2h = {"rows": int(k), "ms_per_row": dt / k * 1e3, "GB/s": k * row_bytes / dt / 1e9,
+               "pcie_inclusive_rows_per_s": 1.0 / (elapsed / args.steps / count + dt / k),
+               "note": "shd_pe_get_rows into host buffers after the timed region (not in value)"}
+
     rows_total = T * args.steps
     value = rows_total / elapsed
     ms_kernel = st["msSparseKernel"] + st["msDirectKernel"] + st["msDenseKernel"]
@@ -163,7 +180,7 @@ def main():
         achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e12
     else:
         bytes_per_launch = algorithmic_bytes_per_row(n, m_arcs, T) * count
-        kname = "k_sparse_rows"
+        kname = "k_batch_rows" if st["batched"] else "k_sparse_rows"
         achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
     out = {
@@ -193,6 +210,8 @@ def main():
     }
     if gather:
         out["allgather"] = gather
+    if d2h:
+        out["d2h"] = d2h
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(top, att, budget_s=args.cpu_budget)
         out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]

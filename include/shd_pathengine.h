@@ -105,6 +105,8 @@ typedef struct ShdPeStats {
     int64_t denseSweeps;       /* min-plus sweeps (incl. the confirming one)       */
     double denseFlops;         /* executed min-plus work: 2 per (s,u,v) visited,
                                   sweeps (skipped K chunks excluded) + pred pass */
+    int32_t batched;           /* mode 1 runs k_batch_rows (multi-source batches)  */
+    int32_t batchLanes;        /* sources per batch (LB) when batched              */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */
@@ -147,6 +149,17 @@ int shd_pe_compute_positions(ShdPe* pe, int32_t start, int32_t count);
  * the direct-edge values (_topology_lookupDirectPath, topology.c:1877-1927). */
 int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double* rel,
                    int32_t* hops, int32_t* pred, uint8_t* flags);
+
+/* Bulk copy of table rows by position [start, start+count) into caller
+ * buffers laid out row-major (count x T, attached order), same fields and
+ * values as shd_pe_get_row; any pointer may be NULL.  Rows not yet computed
+ * are computed first.  The copy streams through the engine's pinned staging
+ * buffers (DMA of the next block overlaps the host copy of the current one),
+ * so a host row store filled after shd_pe_compute_all (topology.c's cache
+ * inserts, :1805-1864) pays one pass at PCIe rate instead of one
+ * synchronous transfer per field per row. */
+int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
+                    int32_t* hops, int32_t* pred, uint8_t* flags);
 
 /* Copy rows [start, start+count) (table positions) of the device table into
  * caller DEVICE buffers (e.g. an RCCL all-gather staging area).  Row-major,

@@ -29,6 +29,10 @@ struct ShdPe {
     int device = 0;
     int numCUs = 256;
     hipStream_t stream = nullptr;
+    hipStream_t copyStream = nullptr;     // D2H of rows (shd_pe_get_rows)
+    unsigned char* stage[2] = {nullptr, nullptr};   // pinned host staging
+    size_t stageBytes = 0;
+    std::mutex copyMu;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evA = nullptr, evB = nullptr;
     std::vector<void*> allocs;
     DevGraph dg{};
@@ -210,6 +214,8 @@ static void configure(ShdPe* pe) {
     if (!(b.delta > 0)) b.delta = 1.0;
     pe->bcfg = b;
     if (pe->batched) pe->stats.deltaUsed = b.delta;
+    pe->stats.batched = pe->batched ? 1 : 0;
+    pe->stats.batchLanes = pe->batched ? b.lb : 0;
 }
 
 // BFS visit rank of every table position (components in vertex order):
@@ -679,6 +685,9 @@ extern "C" int shd_pe_compute_rows(ShdPe* pe, const int32_t* src, int32_t count)
     return compute_positions_locked(pe, pos.data(), count);
 }
 
+static int get_rows_staged(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
+                           int32_t* hops, int32_t* pred, uint8_t* flags);
+
 extern "C" int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double* rel,
                               int32_t* hops, int32_t* pred, uint8_t* flags) {
     if (!pe || srcVertex < 0 || srcVertex >= pe->hg.n) return SHD_PE_EINVAL;
@@ -692,14 +701,96 @@ extern "C" int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double*
             if (rc) return rc;
         }
     }
-    if (hipSetDevice(pe->device) != hipSuccess) return SHD_PE_EHIP;
-    const size_t T = pe->attached.size(), off = (size_t)p * T;
-    if (lat) HIPCHK(hipMemcpy(lat, pe->tab.lat + off, T * 8, hipMemcpyDeviceToHost));
-    if (rel) HIPCHK(hipMemcpy(rel, pe->tab.rel + off, T * 8, hipMemcpyDeviceToHost));
-    if (hops) HIPCHK(hipMemcpy(hops, pe->tab.hops + off, T * 4, hipMemcpyDeviceToHost));
-    if (pred) HIPCHK(hipMemcpy(pred, pe->tab.pred + off, T * 4, hipMemcpyDeviceToHost));
-    if (flags) HIPCHK(hipMemcpy(flags, pe->tab.flags + off, T, hipMemcpyDeviceToHost));
-    return SHD_PE_OK;
+    return get_rows_staged(pe, p, 1, lat, rel, hops, pred, flags);
+}
+
+// Rows [start, start+count) -> caller host buffers through two pinned
+// staging buffers: block b's five field copies run on copyStream while the
+// host copies block b-1 out of the other buffer.
+static int get_rows_staged(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
+                           int32_t* hops, int32_t* pred, uint8_t* flags) {
+    const size_t T = pe->attached.size();
+    const size_t perRow = T * (8 + 8 + 4 + 4 + 1);
+    std::lock_guard<std::mutex> lk(pe->copyMu);
+    HIPCHK(hipSetDevice(pe->device));
+    if (!pe->copyStream) HIPCHK(hipStreamCreateWithFlags(&pe->copyStream, hipStreamNonBlocking));
+    if (!pe->stage[0]) {
+        const size_t want = std::max<size_t>(perRow, (size_t)32 << 20);
+        for (auto& h : pe->stage) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h), want));
+        pe->stageBytes = want;
+    }
+    const int32_t B = (int32_t)std::max<size_t>(1, pe->stageBytes / perRow);
+    struct Blk { int32_t r0, n; };
+    auto issue = [&](int buf, Blk b) -> int {
+        unsigned char* h = pe->stage[buf];
+        const size_t off = ((size_t)start + b.r0) * T, cells = (size_t)b.n * T;
+        unsigned char* q = h;
+        if (lat) { HIPCHK(hipMemcpyAsync(q, pe->tab.lat + off, cells * 8, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 8; }
+        if (rel) { HIPCHK(hipMemcpyAsync(q, pe->tab.rel + off, cells * 8, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 8; }
+        if (hops) { HIPCHK(hipMemcpyAsync(q, pe->tab.hops + off, cells * 4, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 4; }
+        if (pred) { HIPCHK(hipMemcpyAsync(q, pe->tab.pred + off, cells * 4, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 4; }
+        if (flags) { HIPCHK(hipMemcpyAsync(q, pe->tab.flags + off, cells, hipMemcpyDeviceToHost, pe->copyStream)); }
+        return SHD_PE_OK;
+    };
+    auto drain = [&](int buf, Blk b) {
+        const unsigned char* q = pe->stage[buf];
+        const size_t o = (size_t)b.r0 * T, cells = (size_t)b.n * T;
+        if (lat) { std::memcpy(lat + o, q, cells * 8); q += cells * 8; }
+        if (rel) { std::memcpy(rel + o, q, cells * 8); q += cells * 8; }
+        if (hops) { std::memcpy(hops + o, q, cells * 4); q += cells * 4; }
+        if (pred) { std::memcpy(pred + o, q, cells * 4); q += cells * 4; }
+        if (flags) std::memcpy(flags + o, q, cells);
+    };
+    hipEvent_t done[2];
+    HIPCHK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+    if (hipEventCreateWithFlags(&done[1], hipEventDisableTiming) != hipSuccess) {
+        (void)hipEventDestroy(done[0]);
+        return SHD_PE_EHIP;
+    }
+    int rc = SHD_PE_OK;
+    Blk prev{0, 0};
+    int buf = 0;
+    for (int32_t r0 = 0; r0 < count && rc == SHD_PE_OK; r0 += B) {
+        const Blk cur{r0, std::min(B, count - r0)};
+        if ((rc = issue(buf, cur)) == SHD_PE_OK &&
+            hipEventRecord(done[buf], pe->copyStream) != hipSuccess)
+            rc = SHD_PE_EHIP;
+        if (rc == SHD_PE_OK && prev.n) {
+            if (hipEventSynchronize(done[buf ^ 1]) != hipSuccess) rc = SHD_PE_EHIP;
+            else drain(buf ^ 1, prev);
+        }
+        prev = cur;
+        buf ^= 1;
+    }
+    if (rc == SHD_PE_OK && prev.n) {
+        if (hipEventSynchronize(done[buf ^ 1]) != hipSuccess) rc = SHD_PE_EHIP;
+        else drain(buf ^ 1, prev);
+    }
+    (void)hipStreamSynchronize(pe->copyStream);
+    (void)hipEventDestroy(done[0]);
+    (void)hipEventDestroy(done[1]);
+    return rc;
+}
+
+extern "C" int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
+                               int32_t* hops, int32_t* pred, uint8_t* flags) {
+    if (!pe || start < 0 || count < 0 || (int64_t)start + count > (int64_t)pe->attached.size())
+        return SHD_PE_EINVAL;
+    if (pred && !pe->opt.storePred) return SHD_PE_EINVAL;
+    if (count == 0) return SHD_PE_OK;
+    bool all = true;
+    for (int32_t i = start; i < start + count; ++i) all = all && pe->rowDone[i];
+    if (!all) {
+        std::lock_guard<std::mutex> lk(pe->mu);
+        std::vector<int32_t> todo;
+        for (int32_t i = start; i < start + count; ++i)
+            if (!pe->rowDone[i]) todo.push_back(i);
+        if (!todo.empty()) {
+            int rc = compute_positions_locked(pe, todo.data(), (int32_t)todo.size());
+            if (rc) return rc;
+        }
+    }
+    return get_rows_staged(pe, start, count, lat, rel, hops, pred, flags);
 }
 
 extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, double* dLat,
@@ -734,6 +825,9 @@ extern "C" void shd_pe_destroy(ShdPe* pe) {
     if (pe->evA) (void)hipEventDestroy(pe->evA);
     if (pe->evB) (void)hipEventDestroy(pe->evB);
     if (pe->stream) (void)hipStreamDestroy(pe->stream);
+    if (pe->copyStream) (void)hipStreamDestroy(pe->copyStream);
+    for (unsigned char* h : pe->stage)
+        if (h) (void)hipHostFree(h);
     delete pe;
 }
 
@@ -765,6 +859,8 @@ extern "C" int shd_pe_reset_stats(ShdPe* pe) {
     pe->stats.nArcs = keep.nArcs;
     pe->stats.nAttached = keep.nAttached;
     pe->stats.deltaUsed = keep.deltaUsed;
+    pe->stats.batched = keep.batched;
+    pe->stats.batchLanes = keep.batchLanes;
     return SHD_PE_OK;
 }
 

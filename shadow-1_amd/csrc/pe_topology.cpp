@@ -19,7 +19,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
-#include <unordered_map>
+#include <memory>
 #include <vector>
 
 #include "pe_graph.hpp"
@@ -28,12 +28,25 @@
 const shdpe::HostGraph* shd_pe_host_graph(const ShdPe* pe);
 int32_t shd_pe_position(const ShdPe* pe, int32_t v);
 
+// Dense host row store, replacing the reference's
+// two-level GHashTable<src, GHashTable<dst, Path*>> (topology.c:1284-1386,
+// path.c:13-38): one row per attached SOURCE ordinal, allocated on its first
+// insert, with a state byte per attached DESTINATION ordinal (0 absent,
+// 1 stored, 2 stored + isDirect) and the Path fields side by side.  Lookups
+// and the should-store test are two array reads instead of two hash probes
+// under rwlocks; a row insert is a sequential pass.  Semantics are the
+// reference's, entry for entry.
 namespace {
-struct Path {                       // src/main/routing/path.c:13-21
-    int32_t isDirect;
-    int32_t src, dst;
-    double latency, reliability;
-    int64_t packetCount;
+struct PathRow {
+    std::vector<double> lat, rel;
+    std::vector<int64_t> packets;
+    std::vector<uint8_t> state;
+    explicit PathRow(size_t T) : lat(T), rel(T), packets(T, 0), state(T, 0) {}
+};
+struct PathRef {                    // a cached Path: row + destination ordinal
+    PathRow* row = nullptr;
+    int32_t j = -1;
+    explicit operator bool() const { return row != nullptr; }
 };
 }  // namespace
 
@@ -41,7 +54,8 @@ struct ShdTopology {
     ShdPe* pe = nullptr;
     const shdpe::HostGraph* g = nullptr;
     int32_t prefersDirectPaths = 0;
-    std::unordered_map<uint64_t, Path> cache;
+    std::vector<std::unique_ptr<PathRow>> rows;   // by attached ordinal of the source
+    int64_t cacheSize = 0;
     double minimumPathLatency = 0.0;
     int64_t rowsComputed = 0;
     bool allComputed = false;
@@ -51,13 +65,12 @@ struct ShdTopology {
     std::mutex mu;
 };
 
-static inline uint64_t key(int32_t s, int32_t d) {
-    return ((uint64_t)(uint32_t)s << 32) | (uint32_t)d;
-}
-
-static Path* cache_get(ShdTopology* t, int32_t s, int32_t d) {
-    auto it = t->cache.find(key(s, d));
-    return it == t->cache.end() ? nullptr : &it->second;
+static PathRef cache_get(const ShdTopology* t, int32_t s, int32_t d) {
+    const int32_t ps = shd_pe_position(t->pe, s), pd = shd_pe_position(t->pe, d);
+    if (ps < 0 || pd < 0) return PathRef{};
+    PathRow* r = t->rows[ps].get();
+    if (!r || !r->state[pd]) return PathRef{};
+    return PathRef{r, pd};
 }
 
 static bool should_store(ShdTopology* t, bool isDirect, int32_t s, int32_t d) {
@@ -70,7 +83,14 @@ static bool should_store(ShdTopology* t, bool isDirect, int32_t s, int32_t d) {
 static void store_path(ShdTopology* t, bool isDirect, int32_t s, int32_t d, double lat,
                        double rel) {
     if (!should_store(t, isDirect, s, d)) return;
-    t->cache[key(s, d)] = Path{isDirect ? 1 : 0, s, d, lat, rel, 0};
+    const int32_t ps = shd_pe_position(t->pe, s), pd = shd_pe_position(t->pe, d);
+    auto& row = t->rows[ps];
+    if (!row) row.reset(new PathRow(t->attached.size()));
+    row->lat[pd] = lat;
+    row->rel[pd] = rel;
+    row->packets[pd] = 0;
+    row->state[pd] = isDirect ? 2 : 1;
+    t->cacheSize++;
     if (t->minimumPathLatency == 0 || lat < t->minimumPathLatency) t->minimumPathLatency = lat;
 }
 
@@ -99,11 +119,11 @@ static bool compute_source_paths(ShdTopology* t, int32_t s, int32_t d) {
     return allSuccess;
 }
 
-static Path* get_path_entry(ShdTopology* t, int32_t s, int32_t d) {
+static PathRef get_path_entry(ShdTopology* t, int32_t s, int32_t d) {
     const shdpe::HostGraph* g = t->g;
-    if (s < 0 || s >= g->n || d < 0 || d >= g->n) return nullptr;
-    if (shd_pe_position(t->pe, s) < 0 || shd_pe_position(t->pe, d) < 0) return nullptr;
-    Path* p = cache_get(t, s, d);
+    if (s < 0 || s >= g->n || d < 0 || d >= g->n) return PathRef{};
+    if (shd_pe_position(t->pe, s) < 0 || shd_pe_position(t->pe, d) < 0) return PathRef{};
+    PathRef p = cache_get(t, s, d);
     if (!p && !g->directed) p = cache_get(t, d, s);
     if (!p) {
         bool success;
@@ -136,6 +156,7 @@ extern "C" int shd_topology_new(ShdPe* pe, int32_t prefersDirectPaths, ShdTopolo
     t->rlat.resize(T);
     t->rrel.resize(T);
     t->rflags.resize(T);
+    t->rows.resize(T);
     *out = t;
     return SHD_PE_OK;
 }
@@ -145,15 +166,15 @@ extern "C" void shd_topology_free(ShdTopology* t) { delete t; }
 extern "C" double shd_topology_get_latency(ShdTopology* t, int32_t s, int32_t d) {
     if (!t) return -1.0;
     std::lock_guard<std::mutex> lk(t->mu);
-    Path* p = get_path_entry(t, s, d);
-    return p ? p->latency : -1.0;
+    const PathRef p = get_path_entry(t, s, d);
+    return p ? p.row->lat[p.j] : -1.0;
 }
 
 extern "C" double shd_topology_get_reliability(ShdTopology* t, int32_t s, int32_t d) {
     if (!t) return -1.0;
     std::lock_guard<std::mutex> lk(t->mu);
-    Path* p = get_path_entry(t, s, d);
-    return p ? p->reliability : -1.0;
+    const PathRef p = get_path_entry(t, s, d);
+    return p ? p.row->rel[p.j] : -1.0;
 }
 
 extern "C" int shd_topology_is_routable(ShdTopology* t, int32_t s, int32_t d) {
@@ -163,21 +184,22 @@ extern "C" int shd_topology_is_routable(ShdTopology* t, int32_t s, int32_t d) {
 extern "C" int shd_topology_increment_path_packet_counter(ShdTopology* t, int32_t s, int32_t d) {
     if (!t) return -1;
     std::lock_guard<std::mutex> lk(t->mu);
-    Path* p = get_path_entry(t, s, d);
+    const PathRef p = get_path_entry(t, s, d);
     if (!p) return -1;
-    p->packetCount++;
+    p.row->packets[p.j]++;
     return 0;
 }
 
 extern "C" int shd_topology_cached(const ShdTopology* t, int32_t s, int32_t d, double* lat,
                                    double* rel, int32_t* isDirect, int64_t* packetCount) {
     if (!t) return 0;
-    auto it = t->cache.find(key(s, d));
-    if (it == t->cache.end()) return 0;
-    if (lat) *lat = it->second.latency;
-    if (rel) *rel = it->second.reliability;
-    if (isDirect) *isDirect = it->second.isDirect;
-    if (packetCount) *packetCount = it->second.packetCount;
+    if (s < 0 || s >= t->g->n || d < 0 || d >= t->g->n) return 0;
+    const PathRef p = cache_get(t, s, d);
+    if (!p) return 0;
+    if (lat) *lat = p.row->lat[p.j];
+    if (rel) *rel = p.row->rel[p.j];
+    if (isDirect) *isDirect = p.row->state[p.j] == 2 ? 1 : 0;
+    if (packetCount) *packetCount = p.row->packets[p.j];
     return 1;
 }
 
@@ -186,7 +208,7 @@ extern "C" double shd_topology_min_latency(const ShdTopology* t) {
 }
 
 extern "C" int64_t shd_topology_cache_size(const ShdTopology* t) {
-    return t ? (int64_t)t->cache.size() : 0;
+    return t ? t->cacheSize : 0;
 }
 
 extern "C" int64_t shd_topology_rows_computed(const ShdTopology* t) {

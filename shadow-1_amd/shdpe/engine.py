@@ -23,7 +23,7 @@ F_FAILED = F_UNREACHABLE | F_NOEDGE
 EXPORTS = [
     "shd_pe_default_options", "shd_pe_create", "shd_pe_destroy", "shd_pe_strerror",
     "shd_pe_is_complete", "shd_pe_num_attached", "shd_pe_attached", "shd_pe_compute_all",
-    "shd_pe_compute_rows", "shd_pe_compute_positions", "shd_pe_get_row",
+    "shd_pe_compute_rows", "shd_pe_compute_positions", "shd_pe_get_row", "shd_pe_get_rows",
     "shd_pe_copy_rows_device", "shd_pe_synchronize", "shd_pe_get_stats", "shd_pe_reset_stats",
     "shd_pe_direct_path", "shd_pe_self_path", "shd_pe_adjacent", "shd_topology_new",
     "shd_topology_free", "shd_topology_get_latency", "shd_topology_get_reliability",
@@ -53,7 +53,8 @@ class Stats(C.Structure):
                 ("mode", C.c_int32), ("isComplete", C.c_int32), ("nVertices", C.c_int32),
                 ("nArcs", C.c_int64), ("nAttached", C.c_int32), ("deltaUsed", C.c_double),
                 ("msDenseKernel", C.c_double), ("launchesDense", C.c_int64),
-                ("denseSweeps", C.c_int64), ("denseFlops", C.c_double)]
+                ("denseSweeps", C.c_int64), ("denseFlops", C.c_double),
+                ("batched", C.c_int32), ("batchLanes", C.c_int32)]
 
 
 class EngineError(RuntimeError):
@@ -87,6 +88,7 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_compute_rows": (C.c_int, [vp, vp, i32]),
         "shd_pe_compute_positions": (C.c_int, [vp, i32, i32]),
         "shd_pe_get_row": (C.c_int, [vp, i32, vp, vp, vp, vp, vp]),
+        "shd_pe_get_rows": (C.c_int, [vp, i32, i32, vp, vp, vp, vp, vp]),
         "shd_pe_copy_rows_device": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
         "shd_pe_synchronize": (C.c_int, [vp]),
         "shd_pe_get_stats": (C.c_int, [vp, vp]),
@@ -184,6 +186,16 @@ class Engine:
         pred = np.empty(T, np.int32) if self.store_pred else None
         self._chk(self._lib.shd_pe_get_row(self.h, int(src), _p(lat), _p(rel), _p(hops),
                                            _p(pred), _p(flags)), "shd_pe_get_row")
+        return dict(lat=lat, rel=rel, hops=hops, pred=pred, flags=flags)
+
+    def get_rows(self, start: int, count: int):
+        """Rows [start, start+count) by table position, row-major (count x T)."""
+        T = self.T
+        lat = np.empty((count, T)); rel = np.empty((count, T))
+        hops = np.empty((count, T), np.int32); flags = np.empty((count, T), np.uint8)
+        pred = np.empty((count, T), np.int32) if self.store_pred else None
+        self._chk(self._lib.shd_pe_get_rows(self.h, int(start), int(count), _p(lat), _p(rel),
+                                            _p(hops), _p(pred), _p(flags)), "shd_pe_get_rows")
         return dict(lat=lat, rel=rel, hops=hops, pred=pred, flags=flags)
 
     def copy_rows_device(self, start, count, d_lat=0, d_rel=0, d_hops=0, d_flags=0):

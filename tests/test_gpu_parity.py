@@ -123,6 +123,22 @@ def test_shipped_minus_one_edge_ties(E, oracle_mod):
     assert st["rowsExact"] > 0        # 0.005-quantised latencies -> equal-dist ties
 
 
+def test_bulk_get_rows_matches_get_row(E):
+    """shd_pe_get_rows (staged bulk D2H, several staging blocks) returns the
+    same bytes as per-row shd_pe_get_row."""
+    top = G.rgg(3000, seed=21)
+    eng = E.Engine(top, np.arange(top.n))
+    eng.compute_all()
+    blk = eng.get_rows(5, 2990)        # 2990 rows x 3000 x 25 B = 224 MB > 2 x 32 MB staging
+    for i in (0, 1, 1337, 2989):
+        one = eng.get_row(int(eng.attached[5 + i]))
+        for k in ("lat", "rel", "hops", "pred", "flags"):
+            assert np.array_equal(blk[k][i].view(np.uint8), one[k].view(np.uint8)), (i, k)
+    with pytest.raises(E.EngineError):
+        eng.get_rows(2990, 100)
+    eng.close()
+
+
 def test_partial_attached_and_unattached_source(E, oracle_mod):
     top = G.rgg(3000, seed=9)
     att = G.sample_attached(top.n, 700, seed=1)
