@@ -24,6 +24,7 @@
 //   k_direct_rows  complete graphs: direct-edge gather (HBM-bound).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "pe_device.hpp"
@@ -1103,6 +1104,153 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
     }
 }
 
+// k_exact_rows_soa: the same emulation when the whole heap and index2 fit
+// LDS (16 B per vertex: n <= 10240).  Structure-of-arrays heap (key f64,
+// idx i32) so a sift-down level reads both children's keys with one
+// ds_read2_b64 and their ids with one ds_read2_b32 -- one LDS round trip per
+// level, no global branch.  Labels are not carried in the heap: the lanes
+// that push / modify v write P/H/R[v] (global); the pop reads H/R[u] after
+// a workgroup release fence (the writes came from other lanes of this wave).
+constexpr int EX_SOA_MAXN = 10240;
+
+__global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevTable tab0,
+                                                               DevScratch sc0,
+                                                               const int32_t* __restrict__ rows,
+                                                               int32_t nRows) {
+    const DevGraph g = global_view(g0);
+    const DevTable tab = global_view(tab0);
+    const DevScratch sc = global_view(sc0);
+    const int n = g.n;
+    const int lane = threadIdx.x;
+    const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
+    double* hkey = reinterpret_cast<double*>(ex_smem);
+    int32_t* hidx = reinterpret_cast<int32_t*>(ex_smem + (size_t)8 * n);
+    int32_t* index2 = hidx + n;
+    double* D = sc.dist + slot;
+    int32_t* H = sc.hops + slot;
+    double* R = sc.rel + slot;
+    int32_t* P = sc.pred + slot;
+    {
+        const size_t m = (size_t)g.rowPtr[n];
+        uint32_t acc = warm_cache(g.rowPtr, (size_t)4 * (n + 1), lane, EX_THREADS);
+        acc ^= warm_cache(g.col, 4 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.lat, 8 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.rel, 8 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.outToIn, 4 * m, lane, EX_THREADS);
+        acc ^= warm_cache(g.isAttached, (size_t)n, lane, EX_THREADS);
+        if (acc == 0x5bd1e995u) D[lane] = 0.0;   // keeps the loads; D is rewritten before use
+    }
+    // lane-0 heap primitives (hole moves; igraph heap.c semantics)
+    auto place = [&](int p, double k, int id) {
+        hkey[p] = k;
+        hidx[p] = id;
+        index2[id] = p + 2;
+    };
+    auto sink_hole = [&](int head, double k, int size) -> int {
+        for (;;) {
+            const int l = 2 * head + 1;
+            if (l >= size) return head;
+            const bool hasR = l + 1 < size;
+            const double kl = hkey[l], kr = hkey[l + 1];   // l + 1 <= n - 1 + 1: inside LDS
+            const int il = hidx[l], ir = hidx[l + 1];
+            const bool useL = !hasR || kl >= kr;
+            const double ck = useL ? kl : kr;
+            if (!(k < ck)) return head;
+            place(head, ck, useL ? il : ir);
+            head = useL ? l : l + 1;
+        }
+    };
+    auto shift_up = [&](int elem, double k, int id) {
+        while (elem > 0) {
+            const int p = ((elem + 1) >> 1) - 1;
+            const double pk = hkey[p];
+            if (k < pk) break;
+            place(elem, pk, hidx[p]);
+            elem = p;
+        }
+        place(elem, k, id);
+    };
+
+    for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
+        const int r = rows[b];
+        const int s = g.attached[r];
+        for (int v = lane; v < n; v += EX_THREADS) index2[v] = 0;
+        if (lane == 0) {
+            place(0, 0.0, s);
+            H[s] = 0;
+            R[s] = 1.0;
+            P[s] = -1;
+        }
+        __syncthreads();
+        int size = 1;                     // uniform (every lane tracks it)
+        int toReach = g.T;
+        while (size > 0 && toReach > 0) {
+            // pop: top known before the sift-down, its arc range loads meanwhile
+            const int u = __builtin_amdgcn_readfirstlane(hidx[0]);
+            const double mind = -hkey[0];
+            // labels of u were written by lanes of this wave: order their
+            // stores, then fetch labels + arc range together (one round trip
+            // that overlaps the sift-down)
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
+            const int att = g.isAttached[u];
+            const int hu = H[u];
+            const double ru = R[u];
+            size -= 1;
+            if (lane == 0) {
+                if (size > 0) {
+                    const double lk = hkey[size];
+                    const int li = hidx[size];
+                    const int pos = sink_hole(0, lk, size);
+                    place(pos, lk, li);
+                }
+                index2[u] = 1;
+                D[u] = mind;
+            }
+            if (att) --toReach;
+            for (int base = a0; base < a1; base += 64) {
+                const int a = base + lane;
+                const bool valid = a < a1;
+                const int ac = valid ? a : a0;
+                const int v = g.col[ac];
+                const double w = g.lat[ac];
+                const double rw = g.rel[ac];
+                const int ia = g.outToIn[ac];
+                const int st = valid ? index2[v] : 1;
+                const double alt = mind + w;
+                int need = 0;
+                if (st == 0) need = 1;
+                else if (st >= 2) need = (alt < -hkey[st - 2]) ? 2 : 0;
+                const int nh = hu + 1;
+                const double nr = ru * rw;
+                if (need) { P[v] = ia; H[v] = nh; R[v] = nr; }
+                unsigned long long mask = __ballot(need != 0);
+                while (mask) {
+                    const int k = __builtin_ctzll(mask);
+                    mask &= mask - 1;
+                    const int vk = __builtin_amdgcn_readlane(v, k);
+                    const int nk = __builtin_amdgcn_readlane(need, k);
+                    const double ak = __shfl(alt, k, 64);
+                    if (lane == 0) {
+                        if (nk == 1) {            // igraph_2wheap_push_with_index
+                            shift_up(size, -ak, vk);
+                        } else {                  // igraph_2wheap_modify: sink, then shift_up
+                            const int pos = index2[vk] - 2;
+                            shift_up(sink_hole(pos, -ak, size), -ak, vk);
+                        }
+                    }
+                    size += nk == 1 ? 1 : 0;
+                }
+            }
+        }
+        __syncthreads();
+        write_row(g, tab, r, s,
+                  [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
+                  [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_direct_rows: complete graphs (and prefersDirectPaths pairs): row entry =
 // _topology_lookupDirectPath (topology.c:1877-1927).
@@ -1200,6 +1348,14 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
     if (nRows <= 0) return;
     if (grid > nRows) grid = nRows;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (g.n <= EX_SOA_MAXN && !std::getenv("SHDPE_EXACT_AOS") && !std::getenv("SHDPE_EXACT_HC")) {
+        const int sb = (int)(((size_t)16 * g.n + 15) & ~(size_t)15);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows_soa),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, sb);
+        hipLaunchKernelGGL(k_exact_rows_soa, dim3(grid), dim3(EX_THREADS), sb, st, g, tab, sc,
+                           dRows, nRows);
+        return;
+    }
     const int bytes = (int)(((size_t)24 * hc + (ldsIndex ? (size_t)4 * g.n : 0) + 15) & ~(size_t)15);
     if (ldsIndex) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<true>),
