@@ -24,13 +24,22 @@ struct alignas(16) Arc {
     int32_t pad;
 };
 
+// 12-byte packed arc (col, lat as two dwords): one global_load_dwordx3 per
+// arc and a single 12-B-per-arc copy of the graph for the sparse kernel's
+// relax loop and predecessor pass (smaller L2 footprint than AoS 16 B + SoA).
+struct alignas(4) Arc3 {
+    int32_t col;
+    uint32_t latLo, latHi;
+};
+
 struct DevGraph {
     int32_t n;
     int32_t T;                 // unique attached vertices (= targets)
     const int32_t* rowPtr;     // [n+1]
     const int32_t* col;        // [nArcs]
     const double* lat;
-    const Arc* arcs;           // [nArcs] AoS copy of (lat, col) for the relax loop
+    const Arc* arcs;           // [nArcs] AoS copy of (lat, col) (batch kernel)
+    const Arc3* arc3;          // [nArcs] packed 12-B (col, lat) for k_sparse_rows
     const double* rel;
     const int32_t* inPtr;      // [n+1] (aliases rowPtr when undirected)
     const int32_t* inCol;

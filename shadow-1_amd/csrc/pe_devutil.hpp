@@ -32,6 +32,7 @@ __device__ __forceinline__ DevGraph global_view(const DevGraph& g0) {
     g.rowPtr = as_global(g0.rowPtr);
     g.col = as_global(g0.col);
     g.arcs = as_global(g0.arcs);
+    g.arc3 = as_global(g0.arc3);
     g.lat = as_global(g0.lat);
     g.rel = as_global(g0.rel);
     g.inPtr = as_global(g0.inPtr);

@@ -313,6 +313,15 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
         Arc* da;
         if ((rc = dev_upload(pe, &da, arcs))) { shd_pe_destroy(pe); return rc; }
         d.arcs = da;
+        std::vector<Arc3> a3(g.col.size());
+        for (size_t a = 0; a < a3.size(); ++a) {
+            uint64_t bits;
+            std::memcpy(&bits, &g.lat[a], 8);
+            a3[a] = Arc3{g.col[a], (uint32_t)bits, (uint32_t)(bits >> 32)};
+        }
+        Arc3* d3;
+        if ((rc = dev_upload(pe, &d3, a3))) { shd_pe_destroy(pe); return rc; }
+        d.arc3 = d3;
     }
     d.rowPtr = rowPtr; d.col = col; d.lat = lat; d.rel = rel; d.outToIn = outToIn;
     d.vrel = vrel; d.selfLat = sl; d.selfRel = sr; d.hasSelf = hs; d.attached = att;

@@ -268,9 +268,9 @@ __device__ __forceinline__ void process_group(const DevGraph& g, const RowCtx<LA
                 for (int k = 0; k < UNRG; ++k) {
                     const int a = ab + k * LPV;
                     ok[k] = a < a1;
-                    const Arc A = g.arcs[ok[k] ? a : ab];
+                    const Arc3 A = g.arc3[ok[k] ? a : ab];
                     xs[k] = A.col;
-                    ws[k] = A.lat;
+                    ws[k] = __hiloint2double((int)A.latHi, (int)A.latLo);
                 }
             }
 #pragma unroll
