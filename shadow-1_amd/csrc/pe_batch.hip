@@ -57,6 +57,14 @@ struct alignas(16) BCtrl {
 
 // Forward reliability fold with vertex factors (topology.c:1430-1462, :1499)
 // along lane l's predecessor chain, multiplied in source -> target order.
+// packed pointer-jumping entry: low word = ancestor J, high word = H
+__device__ __forceinline__ int jh_j(unsigned long long w) { return (int)(uint32_t)w; }
+__device__ __forceinline__ int jh_h(unsigned long long w) { return (int)(uint32_t)(w >> 32); }
+__device__ __forceinline__ void st_jh(unsigned long long* p, int j, int h) {
+    const unsigned long long w = (unsigned long long)(uint32_t)j | ((unsigned long long)(uint32_t)h << 32);
+    __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int LB>
 __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
                                               const double* __restrict__ inRel,
@@ -117,10 +125,9 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
     double* R = as_global(bs.R + slot * SE);
     int32_t* H = as_global(bs.H + slot * SE);
     int32_t* P = as_global(bs.P + slot * SE);
-    int32_t* J0 = as_global(bs.X + slot * 4 * SE);
-    int32_t* J1 = J0 + SE;
-    int32_t* H1 = J1 + SE;
-    int32_t* LV = H1 + SE;
+    int32_t* const X = as_global(bs.X + slot * 4 * SE);
+    unsigned long long* JH = reinterpret_cast<unsigned long long*>(X);   // 2 SE words
+    int32_t* LV = X + 2 * SE;
     int32_t* Q = as_global(bs.queue + slot * NS);
 
     for (int b = blockIdx.x; b < nBatches; b += gridDim.x) {
@@ -421,8 +428,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                     const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
                     if (!root[v] && dvb[v] != INF_BITS && cnt[v] != 1) amb = true;
                     P[e] = tree ? ba[v] : -1;
-                    J0[e] = tree ? bu[v] : vv;
-                    H[e] = tree ? 1 : 0;
+                    st_jh(&JH[e], tree ? bu[v] : vv, tree ? 1 : 0);
                 }
             }
         }
@@ -444,43 +450,49 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         const long long tPh2 = dbg ? (long long)clock64() : 0;
 
         // ================= 3. hop counts: pointer jumping ====================
-        // invariant: H[e] = tree distance from v to J[e]; roots point to
-        // themselves with 0.  Double-buffered rounds until no pointer moves.
+        // JH[e] = (J, H) packed in one 8-B word: H = tree distance from v to
+        // its ancestor J; roots (and unreached entries) are (v, 0).  Jumping
+        // is in place: every read sees SOME consistent pair (single 8-B
+        // accesses), each a valid (ancestor, distance), so mixing old and new
+        // values only jumps further.  Entries that already point at a root
+        // are final and store ~H (negative): later rounds skip them without
+        // touching their parent, and children jump straight to the root.
         int rounds = 0;
-        int32_t* Jc = J0;
-        int32_t* Jn = J1;
-        int32_t* Hc = H;
-        int32_t* Hn = H1;
         for (;;) {
             int ch = 0, dmax = 0;
             for (size_t e0 = (size_t)tid * 4; e0 < NE; e0 += (size_t)NT * 4) {
-                int j[4], h[4], jj[4], hj[4];
+                unsigned long long p[4], q[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const size_t e = e0 + k;
-                    j[k] = e < NE ? ld_wg(&Jc[e]) : 0;
-                    h[k] = e < NE ? ld_wg(&Hc[e]) : 0;
+                    p[k] = e < NE ? ld_wg(&JH[e]) : 0ull;
                 }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const size_t e = e0 + k;
                     const int v = (int)(e / LB), ll = (int)(e % LB);
-                    if (e < NE && j[k] != v) {
-                        jj[k] = ld_wg(&Jc[(size_t)j[k] * LB + ll]);
-                        hj[k] = ld_wg(&Hc[(size_t)j[k] * LB + ll]);
-                    } else {
-                        jj[k] = j[k];
-                        hj[k] = 0;
-                    }
+                    const int j = jh_j(p[k]), h = jh_h(p[k]);
+                    const bool live = e < NE && j != v && h >= 0;
+                    q[k] = live ? ld_wg(&JH[(size_t)j * LB + ll]) : p[k];
                 }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const size_t e = e0 + k;
                     if (e >= NE) continue;
-                    Jn[e] = jj[k];
-                    Hn[e] = h[k] + hj[k];
-                    if (jj[k] != j[k]) ch = 1;
-                    dmax = max(dmax, h[k] + hj[k]);
+                    const int v = (int)(e / LB);
+                    const int j = jh_j(p[k]), h = jh_h(p[k]);
+                    if (j == v) continue;                          // root / unreached
+                    if (h < 0) {                                   // final
+                        dmax = max(dmax, ~h);
+                        continue;
+                    }
+                    const int jj = jh_j(q[k]), hj = jh_h(q[k]);
+                    int nh;
+                    if (jj == j) nh = ~h;                          // parent is a root
+                    else if (hj < 0) nh = ~(h + ~hj);              // parent final
+                    else nh = h + hj;
+                    st_jh(&JH[e], jj, nh);
+                    ch = 1;
                 }
             }
             if (ch) ctl->changed = 1;
@@ -490,26 +502,31 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             const int any = ctl->changed;
             __syncthreads();
             if (tid == 0) ctl->changed = 0;
-            int32_t* t1 = Jc; Jc = Jn; Jn = t1;
-            int32_t* t2 = Hc; Hc = Hn; Hn = t2;
             ++rounds;
             if (!any) break;
             if (tid == 0) ctl->maxDepth = 0;
             __syncthreads();
         }
-        // Hc now holds the hop count of every entry (0 for roots/unreached)
         const int maxDepth = ctl->maxDepth;
+        // unpack the hop counts into H (0 for roots / unreached) and, for the
+        // depth-ordered fold, histogram them
+        int32_t* const Hc = H;
+        if (maxDepth <= LMAX) {
+            for (int k = tid; k <= maxDepth + 1; k += NT) hist[k] = 0;
+            __syncthreads();
+        }
+        for (size_t e = tid; e < NE; e += NT) {
+            const int h = jh_h(ld_wg(&JH[e]));
+            const int d = h < 0 ? ~h : 0;
+            Hc[e] = d;
+            if (maxDepth <= LMAX && d > 0) atomicAdd(&hist[d], 1);
+        }
+        fence_wg();
+        __syncthreads();
         const long long tPh3 = dbg ? (long long)clock64() : 0;
 
         // ================= 4. reliability in depth order =====================
         if (maxDepth <= LMAX) {
-            for (int k = tid; k <= maxDepth + 1; k += NT) hist[k] = 0;
-            __syncthreads();
-            for (size_t e = tid; e < NE; e += NT) {
-                const int d = ld_wg(&Hc[e]);
-                if (d > 0) atomicAdd(&hist[d], 1);
-            }
-            __syncthreads();
             if (tid < 64) {
                 // exclusive scan of hist[1..maxDepth] by one wave
                 int carry = 0;
