@@ -43,27 +43,33 @@ def shard(T, rank, world):
     return start, end - start
 
 
-def cpu_baseline(top, att, budget_s=12.0, max_rows=4000):
-    """Time the oracle on a bounded sample of the workload's rows (1 thread)."""
+def cpu_baseline(top, att, budget_s=12.0, max_rows=4000, threads=1):
+    """Time the oracle on a bounded sample of the workload's rows.
+
+    threads=1 matches the reference (graphLock serialises every Dijkstra,
+    topology.c:1747-1781); threads>1 is the generous all-cores CPU bound of
+    SURVEY.md §8(d), one source row per thread."""
     import oracle as O
     O.build()
     og = O.OracleGraph(top)
     rng = np.random.default_rng(0)
     order = rng.permutation(att.shape[0])
     done, t0 = 0, time.perf_counter()
-    chunk = 1                        # grows while rows are cheap (dense rows take seconds)
+    chunk = threads                  # grows while rows are cheap (dense rows take seconds)
     while done < max_rows and time.perf_counter() - t0 < budget_s:
         c0 = time.perf_counter()
         srcs = att[order[done:done + chunk]]
-        og.rows(srcs, att, threads=1)
+        if srcs.shape[0] == 0:
+            break
+        og.rows(srcs, att, threads=threads)
         done += srcs.shape[0]
         if time.perf_counter() - c0 < 0.25 * budget_s / 8:
-            chunk = min(chunk * 2, 64)
+            chunk = min(chunk * 2, 64 * threads)
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "source rows/s", "cores": 1, "kind": "port",
+    return {"value": done / dt, "unit": "source rows/s", "cores": threads, "kind": "port",
             "sample": f"{done} random source rows of the same workload (all {att.shape[0]} "
                       f"targets each), igraph-0.7.1-faithful 2-wheap Dijkstra + "
-                      f"_topology_computePathProperties fold, 1 thread, {dt:.1f} s"}
+                      f"_topology_computePathProperties fold, {threads} thread(s), {dt:.1f} s"}
 
 
 def load_traffic(workload):
@@ -83,6 +89,11 @@ def main():
     ap.add_argument("--allgather", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
+                    help="threads of the all-cores CPU bound (1 = skip; the GPU box's "
+                         "share is 16 CPUs, os.cpu_count() there shows the whole machine)")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="skip the device-copy HBM bandwidth reference")
     ap.add_argument("--d2h-rows", type=int, default=2048,
                     help="rows copied to host buffers through shd_pe_get_row after the timed "
                          "region (PCIe-inclusive rate, reported separately; 0 = off)")
@@ -211,6 +222,11 @@ def main():
         "rows_exact": st["rowsExact"] // max(1, args.steps),
         "ms_exact_per_step": st["msExactKernel"] / max(1, args.steps),
     }
+    if rank == 0 and not args.no_stream:
+        sbw = eng.stream_bandwidth()     # 16-B streaming copy kernel, same device
+        out["roofline"]["stream_GBps"] = sbw
+        if bound == "hbm":
+            out["roofline"]["frac_of_stream"] = achieved / sbw
     if gather:
         out["allgather"] = gather
     if d2h:
@@ -218,6 +234,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(top, att, budget_s=args.cpu_budget)
         out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+        if args.cpu_threads > 1:
+            allc = cpu_baseline(top, att, budget_s=args.cpu_budget / 2, threads=args.cpu_threads)
+            out["cpu_baseline_all_cores"] = allc
+            out["speedup_vs_cpu_all_cores"] = value / allc["value"]
     eng.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -171,6 +171,12 @@ int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count,
 /* Wait for outstanding device work of this engine. */
 int shd_pe_synchronize(ShdPe* pe);
 
+/* Measurement helper (not on the path): achievable HBM bandwidth of this
+ * engine's device, a 16-B streaming copy of `bytes` (read + write counted),
+ * averaged over `iters` launches on the engine's stream.  SURVEY.md §8(d)
+ * asks for it beside the spec peak; no reference counterpart. */
+int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbps);
+
 int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out);
 int shd_pe_reset_stats(ShdPe* pe);
 

@@ -65,6 +65,29 @@ __device__ __forceinline__ void st_jh(unsigned long long* p, int j, int h) {
     __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Wave-aggregated counter add: the lanes of a wave that bump the same
+// counter (depth levels: ~20 distinct keys for 10^6 entries) are merged into
+// one LDS atomic per distinct key instead of serialising 64 same-address
+// atomics.  Returns each participating lane's slot (old value + its rank).
+__device__ __forceinline__ int wave_agg_add(int* ctr, int key, bool act) {
+    unsigned long long pend = __ballot(act);
+    int pos = -1;
+    while (pend) {
+        const int leader = __ffsll((long long)pend) - 1;
+        const int k0 = __shfl(key, leader, 64);
+        const bool mine = act && key == k0 && ((pend >> __lane_id()) & 1ull);
+        const unsigned long long m = __ballot(mine);
+        int base = 0;
+        if ((int)__lane_id() == leader) base = atomicAdd(&ctr[k0], __popcll(m));
+        base = __shfl(base, leader, 64);
+        if (mine)
+            pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        pend &= ~m;
+    }
+    return pos;
+}
+
 template <int LB>
 __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
                                               const double* __restrict__ inRel,
@@ -127,7 +150,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
     int32_t* P = as_global(bs.P + slot * SE);
     int32_t* const X = as_global(bs.X + slot * 4 * SE);
     unsigned long long* JH = reinterpret_cast<unsigned long long*>(X);   // 2 SE words
-    int32_t* LV = X + 2 * SE;
+    int2* LV = reinterpret_cast<int2*>(X + 2 * SE);                     // 2 SE words
     int32_t* Q = as_global(bs.queue + slot * NS);
 
     for (int b = blockIdx.x; b < nBatches; b += gridDim.x) {
@@ -515,11 +538,20 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             for (int k = tid; k <= maxDepth + 1; k += NT) hist[k] = 0;
             __syncthreads();
         }
-        for (size_t e = tid; e < NE; e += NT) {
-            const int h = jh_h(ld_wg(&JH[e]));
-            const int d = h < 0 ? ~h : 0;
-            Hc[e] = d;
-            if (maxDepth <= LMAX && d > 0) atomicAdd(&hist[d], 1);
+        for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
+            int hh[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const size_t e = e0 + (size_t)k * NT;
+                hh[k] = e < NE ? jh_h(ld_wg(&JH[e])) : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const size_t e = e0 + (size_t)k * NT;
+                const int d = hh[k] < 0 ? ~hh[k] : 0;
+                if (e < NE) Hc[e] = d;
+                if (maxDepth <= LMAX) wave_agg_add(hist, d, e < NE && d > 0);
+            }
         }
         fence_wg();
         __syncthreads();
@@ -545,23 +577,50 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                 if (tid == 0) { hist[maxDepth + 1] = carry; cur[maxDepth + 1] = carry; }
             }
             __syncthreads();
-            for (size_t e = tid; e < NE; e += NT) {
-                const int d = ld_wg(&Hc[e]);
-                if (d > 0) {
-                    const int pos = atomicAdd(&cur[d], 1);
-                    LV[pos] = (int)e;
+            // counting-sort scatter: LV[pos] = (entry, its tree in-arc)
+            for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
+                int dd[4], aa[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const size_t e = e0 + (size_t)k * NT;
+                    dd[k] = e < NE ? ld_wg(&Hc[e]) : 0;
+                    aa[k] = e < NE ? ld_wg(&P[e]) : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int pos = wave_agg_add(cur, dd[k], dd[k] > 0);
+                    if (pos >= 0) LV[pos] = make_int2((int)(e0 + (size_t)k * NT), aa[k]);
                 }
             }
             fence_wg();
             __syncthreads();
+            // level by level; four entries per thread in flight (the level
+            // loop is a chain of dependent gathers, latency-bound otherwise)
             for (int d = 1; d <= maxDepth; ++d) {
                 const int q0 = hist[d], q1 = hist[d + 1];
-                for (int q = q0 + tid; q < q1; q += NT) {
-                    const int e = ld_wg(&LV[q]);
-                    const int ll = e % LB;
-                    const int a = ld_wg(&P[e]);
-                    const int x = g.inCol[a];
-                    R[e] = ld_wg(&R[(size_t)x * LB + ll]) * g.inRel[a];
+                for (int qb = q0 + tid; qb < q1; qb += NT * 4) {
+                    int2 ea[4];
+                    int xs[4];
+                    double rr[4], rp[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int q = qb + k * NT;
+                        ea[k] = q < q1 ? LV[q] : make_int2(-1, 0);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int a = ea[k].x >= 0 ? ea[k].y : 0;
+                        xs[k] = g.inCol[a];
+                        rr[k] = g.inRel[a];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int ll = (ea[k].x >= 0 ? ea[k].x : 0) % LB;
+                        rp[k] = ld_wg(&R[(size_t)xs[k] * LB + ll]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (ea[k].x >= 0) R[ea[k].x] = rp[k] * rr[k];
                 }
                 fence_wg();
                 __syncthreads();

@@ -817,6 +817,53 @@ extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, 
     return SHD_PE_OK;
 }
 
+// Streaming copy for the achievable-HBM reference: 16-B
+// loads and stores, grid-stride, enough workgroups to fill all 8 XCDs.
+__global__ __launch_bounds__(256) void k_stream_copy(const uint4* __restrict__ a,
+                                                      uint4* __restrict__ b, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 x0 = a[i], x1 = a[i + stride], x2 = a[i + 2 * stride], x3 = a[i + 3 * stride];
+        b[i] = x0;
+        b[i + stride] = x1;
+        b[i + 2 * stride] = x2;
+        b[i + 3 * stride] = x3;
+    }
+    for (; i < n; i += stride) b[i] = a[i];
+}
+
+extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbps) {
+    if (!pe || !gbps || bytes < (1 << 20) || iters < 1) return SHD_PE_EINVAL;
+    HIPCHK(hipSetDevice(pe->device));
+    const size_t n = (size_t)bytes / 16;
+    void *a = nullptr, *b = nullptr;
+    if (hipMalloc(&a, n * 16) != hipSuccess) return SHD_PE_ENOMEM;
+    if (hipMalloc(&b, n * 16) != hipSuccess) { (void)hipFree(a); return SHD_PE_ENOMEM; }
+    int rc = SHD_PE_OK;
+    const int grid = pe->numCUs * 8;
+    if (hipMemsetAsync(a, 0, n * 16, pe->stream) != hipSuccess) rc = SHD_PE_EHIP;
+    if (!rc) {
+        hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, pe->stream, (const uint4*)a,
+                           (uint4*)b, n);   // warm-up
+        (void)hipEventRecord(pe->evA, pe->stream);
+        for (int i = 0; i < iters; ++i)
+            hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, pe->stream,
+                               (const uint4*)a, (uint4*)b, n);
+        (void)hipEventRecord(pe->evB, pe->stream);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(pe->stream) != hipSuccess)
+            rc = SHD_PE_EHIP;
+    }
+    if (!rc) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, pe->evA, pe->evB);
+        *gbps = ms > 0.f ? 2.0 * (double)n * 16.0 * iters / (ms * 1e-3) / 1e9 : 0.0;
+    }
+    (void)hipFree(a);
+    (void)hipFree(b);
+    return rc;
+}
+
 extern "C" int shd_pe_synchronize(ShdPe* pe) {
     if (!pe) return SHD_PE_EINVAL;
     HIPCHK(hipSetDevice(pe->device));

@@ -25,6 +25,7 @@ EXPORTS = [
     "shd_pe_is_complete", "shd_pe_num_attached", "shd_pe_attached", "shd_pe_compute_all",
     "shd_pe_compute_rows", "shd_pe_compute_positions", "shd_pe_get_row", "shd_pe_get_rows",
     "shd_pe_copy_rows_device", "shd_pe_synchronize", "shd_pe_get_stats", "shd_pe_reset_stats",
+    "shd_pe_stream_bandwidth",
     "shd_pe_direct_path", "shd_pe_self_path", "shd_pe_adjacent", "shd_topology_new",
     "shd_topology_free", "shd_topology_get_latency", "shd_topology_get_reliability",
     "shd_topology_is_routable", "shd_topology_increment_path_packet_counter",
@@ -93,6 +94,7 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_synchronize": (C.c_int, [vp]),
         "shd_pe_get_stats": (C.c_int, [vp, vp]),
         "shd_pe_reset_stats": (C.c_int, [vp]),
+        "shd_pe_stream_bandwidth": (C.c_int, [vp, i64, i32, vp]),
         "shd_pe_direct_path": (C.c_int, [vp, i32, i32, vp, vp]),
         "shd_pe_self_path": (C.c_int, [vp, i32, vp, vp]),
         "shd_pe_adjacent": (C.c_int, [vp, i32, i32]),
@@ -178,6 +180,13 @@ class Engine:
 
     def synchronize(self):
         self._chk(self._lib.shd_pe_synchronize(self.h), "shd_pe_synchronize")
+
+    def stream_bandwidth(self, nbytes: int = 2 << 30, iters: int = 10) -> float:
+        """Achievable HBM GB/s of this engine's device (16-B streaming copy)."""
+        out = C.c_double()
+        self._chk(self._lib.shd_pe_stream_bandwidth(self.h, int(nbytes), int(iters),
+                                                    C.byref(out)), "shd_pe_stream_bandwidth")
+        return out.value
 
     def get_row(self, src: int):
         T = self.T
