@@ -212,6 +212,27 @@ double shd_topology_min_latency(const ShdTopology* top);
 int64_t shd_topology_cache_size(const ShdTopology* top);
 int64_t shd_topology_rows_computed(const ShdTopology* top);
 
+/* ------------------------------------------------------------------------
+ * GraphML ingestion (host only, no GPU work).  Replaces
+ * igraph_read_graph_graphml in _topology_loadGraph (topology.c:371-399) plus
+ * the attribute reads the path needs: edge 'latency' (EANV,
+ * _topology_extractEdgeWeights topology.c:1212-1246), edge / vertex
+ * 'packetloss' (topology.c:402-444, :1442-1462) and the graph string
+ * 'preferdirectpaths' (topology.c:769-790, case-insensitive prefix
+ * true/yes/1).  `buf` is the (decompressed) GraphML text.  Vertex ids follow
+ * <node> order and edge ids <edge> order, as igraph assigns them; a missing or
+ * unparsable number is NaN.  Duplicate node ids or an edge naming an unknown
+ * node -> SHD_PE_EINVAL. */
+typedef struct ShdGraphml ShdGraphml;
+int shd_graphml_parse(const char* buf, int64_t len, ShdGraphml** out);
+/* Fill a ShdPeGraphDesc whose arrays point into `g` (valid until
+ * shd_graphml_free); vertexPacketLoss is NULL when no node 'packetloss' key
+ * exists.  Pass it straight to shd_pe_create. */
+int shd_graphml_describe(const ShdGraphml* g, ShdPeGraphDesc* desc, int32_t* prefersDirectPaths);
+/* The GraphML id string of vertex v (NULL if out of range). */
+const char* shd_graphml_vertex_id(const ShdGraphml* g, int32_t v);
+void shd_graphml_free(ShdGraphml* g);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,417 @@
+// pe_graphml.cpp -- native GraphML -> edge-list ingestion.
+//
+// Replaces what Shadow asks igraph for before the path engine starts:
+//   _topology_loadGraph          topology.c:371-399  igraph_read_graph_graphml
+//   _topology_extractEdgeWeights topology.c:1212-1246 EANV("latency")
+//   edge / vertex 'packetloss'   topology.c:402-444, :1442-1462 (EAN / VAN)
+//   graph 'preferdirectpaths'    topology.c:769-790
+// and produces exactly the ShdPeGraphDesc the engine takes: vertex ids in
+// <node> document order, edge ids in <edge> document order (igraph's GraphML
+// import order), endpoints as written (the engine normalises undirected
+// endpoints like igraph_add_edges), numeric values correctly rounded
+// (strtod), an absent or unparsable value = NaN (topology.c:330-370 treats NaN
+// as "absent").  One pass over the buffer, no DOM: the only per-edge state is
+// the four output arrays, so a 2*10^8-edge tmodel file is parsed at memory
+// speed instead of through igraph's attribute tables.
+//
+// Supported XML: elements, attributes ('...' or "..."), the five predefined
+// entities and numeric character references, comments, processing
+// instructions, DOCTYPE, CDATA.  Namespace prefixes are ignored (GraphML's
+// default namespace is the common case).
+#include <cerrno>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "shd_pathengine.h"
+
+namespace {
+
+struct Key {
+    std::string forKind, name, type, deflt;
+    bool hasDefault = false;
+};
+
+struct Tag {
+    std::string name;                                   // local name
+    std::vector<std::pair<std::string, std::string>> attrs;
+    bool end = false, selfClose = false;
+    const std::string* get(const char* k) const {
+        for (auto& a : attrs)
+            if (a.first == k) return &a.second;
+        return nullptr;
+    }
+};
+
+void append_utf8(std::string& o, unsigned long cp) {
+    if (cp < 0x80) o += (char)cp;
+    else if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 0x3F)); }
+    else if (cp < 0x10000) {
+        o += (char)(0xE0 | (cp >> 12)); o += (char)(0x80 | ((cp >> 6) & 0x3F));
+        o += (char)(0x80 | (cp & 0x3F));
+    } else {
+        o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 0x3F));
+        o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F));
+    }
+}
+
+// XML entity decoding of [p, e) appended to out
+void decode(const char* p, const char* e, std::string& out) {
+    while (p < e) {
+        const char* amp = (const char*)memchr(p, '&', (size_t)(e - p));
+        if (!amp) { out.append(p, e); return; }
+        out.append(p, amp);
+        const char* semi = (const char*)memchr(amp, ';', (size_t)(e - amp));
+        if (!semi) { out.append(amp, e); return; }
+        const std::string ent(amp + 1, semi);
+        if (ent == "lt") out += '<';
+        else if (ent == "gt") out += '>';
+        else if (ent == "amp") out += '&';
+        else if (ent == "quot") out += '"';
+        else if (ent == "apos") out += '\'';
+        else if (!ent.empty() && ent[0] == '#') {
+            const bool hex = ent.size() > 1 && (ent[1] == 'x' || ent[1] == 'X');
+            append_utf8(out, strtoul(ent.c_str() + (hex ? 2 : 1), nullptr, hex ? 16 : 10));
+        } else {
+            out.append(amp, semi + 1);
+        }
+        p = semi + 1;
+    }
+}
+
+inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+std::string local_name(const char* p, const char* e) {
+    const char* colon = p;
+    for (const char* q = p; q < e; ++q)
+        if (*q == ':') colon = q + 1;
+    return std::string(colon, e);
+}
+
+// Python float() semantics on a stripped string; empty/invalid -> NaN
+double parse_num(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && is_space(s[a])) ++a;
+    while (b > a && is_space(s[b - 1])) --b;
+    if (a == b) return NAN;
+    const char* t = s.c_str() + a;            // NUL-terminated after the trailing blanks
+    const size_t len = b - a;
+    const size_t k = (t[0] == '-' || t[0] == '+') ? 1 : 0;
+    if (len > k + 1 && t[k] == '0' && (t[k + 1] == 'x' || t[k + 1] == 'X')) return NAN;   // no hex floats
+    char* end = nullptr;
+    const double v = strtod(t, &end);
+    if (end != t + len) return NAN;
+    return v;
+}
+
+}  // namespace
+
+struct ShdGraphml {
+    int32_t n = 0;
+    int32_t directed = 1;
+    int32_t prefersDirect = 0;
+    bool hasVertexLoss = false;
+    std::vector<int32_t> src, dst;
+    std::vector<double> lat, loss, vloss;
+    std::vector<std::string> ids;
+};
+
+namespace {
+
+class Parser {
+  public:
+    Parser(const char* b, size_t n) : p_(b), e_(b + n) {}
+
+    // next markup item; text before it (raw) is returned through `text`
+    // returns false at end of input; sets err_ on malformed markup
+    bool next(Tag& tag, const char*& t0, const char*& t1) {
+        for (;;) {
+            t0 = p_;
+            const char* lt = (const char*)memchr(p_, '<', (size_t)(e_ - p_));
+            if (!lt) { t1 = e_; p_ = e_; return false; }
+            t1 = lt;
+            p_ = lt + 1;
+            if (p_ >= e_) { err_ = true; return false; }
+            if (*p_ == '?') {                      // processing instruction
+                if (!skip_past("?>")) return false;
+                continue;
+            }
+            if (*p_ == '!') {
+                if (e_ - p_ >= 3 && p_[1] == '-' && p_[2] == '-') {
+                    if (!skip_past("-->")) return false;
+                } else if (e_ - p_ >= 8 && memcmp(p_, "![CDATA[", 8) == 0) {
+                    const char* c0 = p_ + 8;
+                    if (!skip_past("]]>")) return false;
+                    cdata_.append(c0, p_ - 3);
+                } else {                           // DOCTYPE and friends
+                    int depth = 0;
+                    while (p_ < e_ && !(*p_ == '>' && depth == 0)) {
+                        if (*p_ == '[') ++depth;
+                        else if (*p_ == ']') --depth;
+                        ++p_;
+                    }
+                    if (p_ >= e_) { err_ = true; return false; }
+                    ++p_;
+                }
+                continue;
+            }
+            return read_tag(tag);
+        }
+    }
+    bool error() const { return err_; }
+    std::string cdata_;     // CDATA collected since the last clear
+
+  private:
+    bool skip_past(const char* s) {
+        const size_t k = strlen(s);
+        while (p_ + k <= e_) {
+            if (memcmp(p_, s, k) == 0) { p_ += k; return true; }
+            ++p_;
+        }
+        err_ = true;
+        return false;
+    }
+    bool read_tag(Tag& t) {
+        t.attrs.clear();
+        t.end = t.selfClose = false;
+        if (*p_ == '/') { t.end = true; ++p_; }
+        const char* n0 = p_;
+        while (p_ < e_ && !is_space(*p_) && *p_ != '>' && *p_ != '/') ++p_;
+        t.name = local_name(n0, p_);
+        for (;;) {
+            while (p_ < e_ && is_space(*p_)) ++p_;
+            if (p_ >= e_) { err_ = true; return false; }
+            if (*p_ == '>') { ++p_; return true; }
+            if (*p_ == '/') {
+                if (p_ + 1 < e_ && p_[1] == '>') { t.selfClose = true; p_ += 2; return true; }
+                err_ = true;
+                return false;
+            }
+            const char* a0 = p_;
+            while (p_ < e_ && *p_ != '=' && !is_space(*p_) && *p_ != '>') ++p_;
+            const char* a1 = p_;
+            while (p_ < e_ && is_space(*p_)) ++p_;
+            if (p_ >= e_ || *p_ != '=') { err_ = true; return false; }
+            ++p_;
+            while (p_ < e_ && is_space(*p_)) ++p_;
+            if (p_ >= e_ || (*p_ != '"' && *p_ != '\'')) { err_ = true; return false; }
+            const char q = *p_++;
+            const char* v0 = p_;
+            const char* v1 = (const char*)memchr(p_, q, (size_t)(e_ - p_));
+            if (!v1) { err_ = true; return false; }
+            p_ = v1 + 1;
+            std::string val;
+            decode(v0, v1, val);
+            t.attrs.emplace_back(local_name(a0, a1), std::move(val));
+        }
+    }
+    const char* p_;
+    const char* e_;
+    bool err_ = false;
+};
+
+int parse(const char* buf, size_t len, ShdGraphml& g) {
+    Parser ps(buf, len);
+    Tag tag;
+    const char *t0, *t1;
+    std::unordered_map<std::string, Key> keys;
+    std::unordered_map<std::string, int32_t> idIndex;
+    std::vector<std::string> stack;
+    Key* curKey = nullptr;             // inside <key> (for <default>)
+    bool inGraph = false, graphDone = false, keyNodeLoss = false;
+    int ctx = 0;                       // 0 none, 1 graph, 2 node, 3 edge (current owner of <data>)
+    int dataDepth = -1;                // stack depth of an open <data>/<default>
+    std::string text, dataKey;
+    bool inDefault = false;
+    // per-owner attribute values by attribute name (latest wins, like a dict)
+    double eLat = NAN, eLoss = NAN, vLoss = NAN;
+    std::string gPdp;
+    bool gPdpSet = false;
+    std::string eSrc, eDst;
+    struct Pending { size_t edge; std::string src, dst; };
+    std::vector<Pending> pending;
+    // defaults by kind, by name
+    auto deflt = [&](const char* kind, const char* name, double& num, std::string* str,
+                     bool* set) {
+        for (auto& kv : keys) {
+            const Key& k = kv.second;
+            if (k.forKind == kind && k.name == name && k.hasDefault) {
+                if (str) { *str = k.deflt; if (set) *set = true; }
+                else num = parse_num(k.deflt);
+            }
+        }
+    };
+    double defLat = NAN, defLoss = NAN, defVLoss = NAN;   // fixed once <graph> opens
+    auto finish_data = [&]() {
+        auto it = keys.find(dataKey);
+        if (it == keys.end()) return;
+        const Key& k = it->second;
+        if (ctx == 1 && stack.size() == 2 && k.forKind == "graph" && k.name == "preferdirectpaths") {
+            gPdp = text;
+            gPdpSet = true;
+        } else if (ctx == 2) {
+            if (k.name == "packetloss") vLoss = parse_num(text);
+        } else if (ctx == 3) {
+            if (k.name == "latency") eLat = parse_num(text);
+            else if (k.name == "packetloss") eLoss = parse_num(text);
+        }
+    };
+    for (;;) {
+        const bool more = ps.next(tag, t0, t1);
+        if (dataDepth >= 0 && t1 > t0) decode(t0, t1, text);
+        if (!ps.cdata_.empty()) {
+            if (dataDepth >= 0) text += ps.cdata_;
+            ps.cdata_.clear();
+        }
+        if (!more) break;
+        if (!tag.end) {
+            const std::string& nm = tag.name;
+            if (nm == "key") {
+                Key k;
+                if (auto v = tag.get("for")) k.forKind = *v;
+                if (auto v = tag.get("attr.name")) k.name = *v;
+                if (auto v = tag.get("attr.type")) k.type = *v;
+                const std::string id = tag.get("id") ? *tag.get("id") : std::string();
+                if (k.forKind == "node" && k.name == "packetloss") keyNodeLoss = true;
+                curKey = &(keys[id] = k);
+            } else if (nm == "default" && curKey) {
+                inDefault = true;
+                dataDepth = (int)stack.size();
+                text.clear();
+            } else if (nm == "graph" && !graphDone && !inGraph && stack.size() == 1) {
+                inGraph = true;
+                ctx = 1;
+                const std::string* ed = tag.get("edgedefault");
+                g.directed = !ed || *ed == "directed";
+                deflt("graph", "preferdirectpaths", vLoss, &gPdp, &gPdpSet);
+                deflt("edge", "latency", defLat, nullptr, nullptr);
+                deflt("edge", "packetloss", defLoss, nullptr, nullptr);
+                deflt("node", "packetloss", defVLoss, nullptr, nullptr);
+            } else if (inGraph && nm == "node" && stack.size() == 2) {
+                ctx = 2;
+                vLoss = defVLoss;
+                const std::string id = tag.get("id") ? *tag.get("id") : std::string();
+                if (!idIndex.emplace(id, (int32_t)g.ids.size()).second) return SHD_PE_EINVAL;
+                g.ids.push_back(id);
+            } else if (inGraph && nm == "edge" && stack.size() == 2) {
+                ctx = 3;
+                eLat = defLat;
+                eLoss = defLoss;
+                eSrc = tag.get("source") ? *tag.get("source") : std::string();
+                eDst = tag.get("target") ? *tag.get("target") : std::string();
+            } else if (inGraph && nm == "data" && ctx != 0) {
+                dataKey = tag.get("key") ? *tag.get("key") : std::string();
+                dataDepth = (int)stack.size();
+                text.clear();
+            }
+            if (tag.selfClose) {
+                // an empty element: close it right away
+                if (nm == "data" && dataDepth == (int)stack.size()) {
+                    finish_data();
+                    dataDepth = -1;
+                } else if (nm == "default" && inDefault) {
+                    curKey->deflt.clear();
+                    curKey->hasDefault = false;    // ElementTree: text None -> no default
+                    inDefault = false;
+                    dataDepth = -1;
+                }
+                tag.end = true;                    // fall through to the close logic
+            } else {
+                stack.push_back(nm);
+                continue;
+            }
+        } else {
+            if (stack.empty() || stack.back() != tag.name) return SHD_PE_EINVAL;
+            stack.pop_back();
+        }
+        // ---- close of element `tag.name` at depth stack.size() ----
+        const std::string& nm = tag.name;
+        if (nm == "data" && dataDepth == (int)stack.size()) {
+            finish_data();
+            dataDepth = -1;
+        } else if (nm == "default" && inDefault) {
+            curKey->deflt = text;
+            curKey->hasDefault = !text.empty();       // ElementTree: no text -> None
+            inDefault = false;
+            dataDepth = -1;
+        } else if (nm == "key") {
+            curKey = nullptr;
+        } else if (nm == "node" && ctx == 2 && stack.size() == 2) {
+            g.vloss.push_back(vLoss);
+            ctx = 1;
+        } else if (nm == "edge" && ctx == 3 && stack.size() == 2) {
+            // endpoints may name nodes declared later in the document
+            auto a = idIndex.find(eSrc), b = idIndex.find(eDst);
+            if (a == idIndex.end() || b == idIndex.end())
+                pending.push_back({g.src.size(), eSrc, eDst});
+            g.src.push_back(a == idIndex.end() ? -1 : a->second);
+            g.dst.push_back(b == idIndex.end() ? -1 : b->second);
+            g.lat.push_back(eLat);
+            g.loss.push_back(eLoss);
+            ctx = 1;
+        } else if (nm == "graph" && inGraph && stack.size() == 1) {
+            inGraph = false;
+            graphDone = true;
+            ctx = 0;
+        }
+    }
+    if (ps.error() || !stack.empty() || !graphDone) return SHD_PE_EINVAL;
+    for (const auto& pe : pending) {
+        auto a = idIndex.find(pe.src), b = idIndex.find(pe.dst);
+        if (a == idIndex.end() || b == idIndex.end()) return SHD_PE_EINVAL;
+        g.src[pe.edge] = a->second;
+        g.dst[pe.edge] = b->second;
+    }
+    g.n = (int32_t)g.ids.size();
+    g.hasVertexLoss = keyNodeLoss;
+    if (gPdpSet && !gPdp.empty()) {
+        std::string low;
+        for (char c : gPdp) low += (char)tolower((unsigned char)c);
+        g.prefersDirect = low.rfind("true", 0) == 0 || low.rfind("yes", 0) == 0 ||
+                          low.rfind("1", 0) == 0;
+    }
+    return SHD_PE_OK;
+}
+
+}  // namespace
+
+extern "C" int shd_graphml_parse(const char* buf, int64_t len, ShdGraphml** out) {
+    if (!buf || len < 0 || !out) return SHD_PE_EINVAL;
+    *out = nullptr;
+    ShdGraphml* g = new (std::nothrow) ShdGraphml();
+    if (!g) return SHD_PE_ENOMEM;
+    int rc;
+    try {
+        rc = parse(buf, (size_t)len, *g);
+    } catch (const std::bad_alloc&) {
+        rc = SHD_PE_ENOMEM;
+    }
+    if (rc) { delete g; return rc; }
+    *out = g;
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_graphml_describe(const ShdGraphml* g, ShdPeGraphDesc* desc,
+                                    int32_t* prefersDirectPaths) {
+    if (!g || !desc) return SHD_PE_EINVAL;
+    desc->nVertices = g->n;
+    desc->nEdges = (int64_t)g->src.size();
+    desc->directed = g->directed;
+    desc->edgeFrom = g->src.data();
+    desc->edgeTo = g->dst.data();
+    desc->edgeLatency = g->lat.data();
+    desc->edgePacketLoss = g->loss.data();
+    desc->vertexPacketLoss = g->hasVertexLoss ? g->vloss.data() : nullptr;
+    if (prefersDirectPaths) *prefersDirectPaths = g->prefersDirect;
+    return SHD_PE_OK;
+}
+
+extern "C" const char* shd_graphml_vertex_id(const ShdGraphml* g, int32_t v) {
+    if (!g || v < 0 || v >= g->n) return nullptr;
+    return g->ids[(size_t)v].c_str();
+}
+
+extern "C" void shd_graphml_free(ShdGraphml* g) { delete g; }

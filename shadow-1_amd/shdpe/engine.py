@@ -30,7 +30,8 @@ EXPORTS = [
     "shd_topology_free", "shd_topology_get_latency", "shd_topology_get_reliability",
     "shd_topology_is_routable", "shd_topology_increment_path_packet_counter",
     "shd_topology_cached", "shd_topology_min_latency", "shd_topology_cache_size",
-    "shd_topology_rows_computed",
+    "shd_topology_rows_computed", "shd_graphml_parse", "shd_graphml_describe",
+    "shd_graphml_vertex_id", "shd_graphml_free",
 ]
 
 
@@ -108,6 +109,10 @@ def load_library(path: str = LIB_PATH):
         "shd_topology_min_latency": (f64, [vp]),
         "shd_topology_cache_size": (i64, [vp]),
         "shd_topology_rows_computed": (i64, [vp]),
+        "shd_graphml_parse": (C.c_int, [C.c_char_p, i64, vp]),
+        "shd_graphml_describe": (C.c_int, [vp, vp, vp]),
+        "shd_graphml_vertex_id": (C.c_char_p, [vp, i32]),
+        "shd_graphml_free": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -282,3 +287,46 @@ class TopologyShim:
     @property
     def rows_computed(self):
         return self._lib.shd_topology_rows_computed(self.h)
+
+
+def parse_graphml(data, name: str = "topology", with_ids: bool = True):
+    """Native GraphML ingestion (shd_graphml_parse, pe_graphml.cpp): text or
+    bytes (an ``.xz`` path is decompressed here) -> Topology.  Host-only, no
+    GPU needed; the same result as igraph's import order (ids in document
+    order)."""
+    import lzma
+    from .graph import Topology
+    if isinstance(data, str) and not data.lstrip().startswith("<"):
+        with open(data, "rb") as f:
+            raw = f.read()
+        data = lzma.decompress(raw) if str(data).endswith(".xz") else raw
+    if isinstance(data, str):
+        data = data.encode()
+    lib = load_library()
+    h = C.c_void_p()
+    rc = lib.shd_graphml_parse(data, len(data), C.byref(h))
+    if rc:
+        raise EngineError(rc, "shd_graphml_parse")
+    try:
+        d = GraphDesc()
+        pdp = C.c_int32()
+        rc = lib.shd_graphml_describe(h, C.byref(d), C.byref(pdp))
+        if rc:
+            raise EngineError(rc, "shd_graphml_describe")
+        n, m = int(d.nVertices), int(d.nEdges)
+
+        def arr(ptr, ctype, count, dtype):
+            if count == 0 or not ptr:
+                return np.zeros(count, dtype)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(count,)).astype(dtype)
+
+        src = arr(d.edgeFrom, C.c_int32, m, np.int32)
+        dst = arr(d.edgeTo, C.c_int32, m, np.int32)
+        lat = arr(d.edgeLatency, C.c_double, m, np.float64)
+        loss = arr(d.edgePacketLoss, C.c_double, m, np.float64)
+        vloss = arr(d.vertexPacketLoss, C.c_double, n, np.float64) if d.vertexPacketLoss else None
+        ids = [lib.shd_graphml_vertex_id(h, v).decode() for v in range(n)] if with_ids else None
+        return Topology(n=n, directed=bool(d.directed), src=src, dst=dst, latency=lat, loss=loss,
+                        vloss=vloss, ids=ids, prefers_direct=bool(pdp.value), name=name)
+    finally:
+        lib.shd_graphml_free(h)

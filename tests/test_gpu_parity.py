@@ -343,3 +343,20 @@ def test_batched_kernel(E, oracle_mod, case):
     assert st["mode"] == 1 and st["launchesSparse"] >= 1
     if case == "quantized":
         assert st["rowsExact"] > 0
+
+
+def test_native_graphml_to_engine(E, oracle_mod):
+    """§8 f4 end to end: shipped GraphML -> shd_graphml_parse -> shd_pe_create
+    (complete graph: direct rows), and the same file minus one edge (Dijkstra
+    rows), both bit-exact against the oracle."""
+    path = os.path.join(os.path.dirname(__file__), "data", "topology.graphml.xml.xz")
+    top = E.parse_graphml(path)
+    att = np.arange(top.n, dtype=np.int32)
+    st = _check_engine(E, oracle_mod, top, att, sources=att[::7])
+    assert st["mode"] == 2
+    keep = np.ones(top.m, bool)
+    keep[np.flatnonzero(top.src != top.dst)[0]] = False
+    cut = Topology(top.n, top.directed, top.src[keep], top.dst[keep], top.latency[keep],
+                   top.loss[keep], top.vloss)
+    st = _check_engine(E, oracle_mod, cut, att, sources=att[::5])
+    assert st["mode"] != 2
