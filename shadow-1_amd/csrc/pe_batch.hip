@@ -191,11 +191,13 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         // the whole dist[x][0..LB) line anyway) and never improves anything.
         // Lanes at or above the bound keep the vertex pending (deferred);
         // the bound only grows, so such a lane has never been processed at
-        // its current value.  Improvements are PLAIN stores (an atomic must
-        // fetch its line from HBM before it completes, and vmcnt drains in
-        // order, so every later load would wait behind it); a lost update
-        // (two groups improving the same entry at once) is caught by the
-        // Bellman check of pass 2, which re-enters this loop.
+        // its current value.  Improvements are no-return atomic mins at
+        // workgroup scope: the line was just read for the pre-check, so the
+        // atomic resolves in L2, and no update is lost.  (Plain stores lost
+        // ~1 update per batch to concurrent groups, and the Bellman repair
+        // that caught it -- a second relax + predecessor pass -- cost 20% of
+        // the relax phase at C4.)  The Bellman check of pass 2 stays as the
+        // safety net.
         const long long tPh0 = dbg ? (long long)clock64() : 0;
         long long tPh1 = 0;
         int par = 0, phases = 0, repairs = 0;
@@ -300,7 +302,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                             if (x >= 0) {
                                 const unsigned long long nb = d2b(b2d(dub[v]) + ws[v][k]);
                                 if (nb < dx[v][k]) {
-                                    D[(size_t)x * LB + l] = nb;
+                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                                     imp = true;
                                 }
                             }

@@ -352,8 +352,18 @@ def test_native_graphml_to_engine(E, oracle_mod):
     path = os.path.join(os.path.dirname(__file__), "data", "topology.graphml.xml.xz")
     top = E.parse_graphml(path)
     att = np.arange(top.n, dtype=np.int32)
-    st = _check_engine(E, oracle_mod, top, att, sources=att[::7])
-    assert st["mode"] == 2
+    og = oracle_mod.OracleGraph(top)
+    eng = E.Engine(top, att)
+    assert eng.is_complete
+    eng.compute_all()
+    for s in (0, 91, 182):
+        r = eng.get_row(s)
+        assert np.all(r["flags"] == E.F_DIRECT)
+        for t in range(top.n):
+            lat, rel = og.direct(s, t)
+            assert r["lat"][t] == lat and r["rel"][t] == rel
+    assert eng.stats()["mode"] == 2
+    eng.close()
     keep = np.ones(top.m, bool)
     keep[np.flatnonzero(top.src != top.dst)[0]] = False
     cut = Topology(top.n, top.directed, top.src[keep], top.dst[keep], top.latency[keep],
