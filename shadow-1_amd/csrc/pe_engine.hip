@@ -819,16 +819,21 @@ extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, 
 
 // Streaming copy for the achievable-HBM reference: 16-B
 // loads and stores, grid-stride, enough workgroups to fill all 8 XCDs.
-__global__ __launch_bounds__(256) void k_stream_copy(const uint4* __restrict__ a,
-                                                      uint4* __restrict__ b, size_t n) {
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_copy(const v4u* __restrict__ a,
+                                                      v4u* __restrict__ b, size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (; i + 3 * stride < n; i += 4 * stride) {
-        const uint4 x0 = a[i], x1 = a[i + stride], x2 = a[i + 2 * stride], x3 = a[i + 3 * stride];
-        b[i] = x0;
-        b[i + stride] = x1;
-        b[i + 2 * stride] = x2;
-        b[i + 3 * stride] = x3;
+        // non-temporal: the copy streams through, nothing is re-read
+        const v4u x0 = __builtin_nontemporal_load(&a[i]);
+        const v4u x1 = __builtin_nontemporal_load(&a[i + stride]);
+        const v4u x2 = __builtin_nontemporal_load(&a[i + 2 * stride]);
+        const v4u x3 = __builtin_nontemporal_load(&a[i + 3 * stride]);
+        __builtin_nontemporal_store(x0, &b[i]);
+        __builtin_nontemporal_store(x1, &b[i + stride]);
+        __builtin_nontemporal_store(x2, &b[i + 2 * stride]);
+        __builtin_nontemporal_store(x3, &b[i + 3 * stride]);
     }
     for (; i < n; i += stride) b[i] = a[i];
 }
@@ -841,15 +846,15 @@ extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, 
     if (hipMalloc(&a, n * 16) != hipSuccess) return SHD_PE_ENOMEM;
     if (hipMalloc(&b, n * 16) != hipSuccess) { (void)hipFree(a); return SHD_PE_ENOMEM; }
     int rc = SHD_PE_OK;
-    const int grid = pe->numCUs * 8;
+    const int grid = pe->numCUs * env_int("SHDPE_STREAM_WG_PER_CU", 4);
     if (hipMemsetAsync(a, 0, n * 16, pe->stream) != hipSuccess) rc = SHD_PE_EHIP;
     if (!rc) {
-        hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, pe->stream, (const uint4*)a,
-                           (uint4*)b, n);   // warm-up
+        hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, pe->stream, (const v4u*)a,
+                           (v4u*)b, n);   // warm-up
         (void)hipEventRecord(pe->evA, pe->stream);
         for (int i = 0; i < iters; ++i)
             hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, pe->stream,
-                               (const uint4*)a, (uint4*)b, n);
+                               (const v4u*)a, (v4u*)b, n);
         (void)hipEventRecord(pe->evB, pe->stream);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(pe->stream) != hipSuccess)
             rc = SHD_PE_EHIP;
