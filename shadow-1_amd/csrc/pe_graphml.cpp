@@ -22,7 +22,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -35,13 +37,22 @@ struct Key {
     bool hasDefault = false;
 };
 
+// a view into the input buffer
+struct SV {
+    const char* p = nullptr;
+    size_t n = 0;
+    bool eq(const char* s) const { return strlen(s) == n && memcmp(p, s, n) == 0; }
+    bool eq(const SV& o) const { return o.n == n && memcmp(p, o.p, n) == 0; }
+    std::string_view view() const { return std::string_view(p, n); }
+};
+
 struct Tag {
-    std::string name;                                   // local name
-    std::vector<std::pair<std::string, std::string>> attrs;
+    SV name;                                            // local name
+    std::vector<std::pair<SV, SV>> attrs;               // raw (entities not decoded)
     bool end = false, selfClose = false;
-    const std::string* get(const char* k) const {
+    const SV* raw(const char* k) const {
         for (auto& a : attrs)
-            if (a.first == k) return &a.second;
+            if (a.first.eq(k)) return &a.second;
         return nullptr;
     }
 };
@@ -84,11 +95,45 @@ void decode(const char* p, const char* e, std::string& out) {
 
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 
-std::string local_name(const char* p, const char* e) {
+SV local_name(const char* p, const char* e) {
     const char* colon = p;
     for (const char* q = p; q < e; ++q)
         if (*q == ':') colon = q + 1;
-    return std::string(colon, e);
+    return SV{colon, (size_t)(e - colon)};
+}
+
+bool has_amp(const SV& v) { return memchr(v.p, '&', v.n) != nullptr; }
+
+// decoded attribute value ("" when absent)
+std::string attr_str(const Tag& t, const char* k) {
+    std::string out;
+    if (const SV* v = t.raw(k)) decode(v->p, v->p + v->n, out);
+    return out;
+}
+
+// Python float() on the stripped text of a view that ends before a '<' (or
+// the buffer end); empty / invalid -> NaN.  strtod stops at the '<'.
+double parse_num_view(const SV& v) {
+    size_t a = 0, b = v.n;
+    while (a < b && is_space(v.p[a])) ++a;
+    while (b > a && is_space(v.p[b - 1])) --b;
+    if (a == b) return NAN;
+    const char* t = v.p + a;
+    const size_t len = b - a;
+    const size_t k = (t[0] == '-' || t[0] == '+') ? 1 : 0;
+    if (len > k + 1 && t[k] == '0' && (t[k + 1] == 'x' || t[k + 1] == 'X')) return NAN;   // no hex floats
+    if (len > 64) {                         // long text: bounded copy keeps strtod inside the view
+        const std::string c(t, len);
+        char* end = nullptr;
+        const double x = strtod(c.c_str(), &end);
+        return end == c.c_str() + len ? x : NAN;
+    }
+    char tmp[72];
+    memcpy(tmp, t, len);
+    tmp[len] = 0;
+    char* end = nullptr;
+    const double x = strtod(tmp, &end);
+    return end == tmp + len ? x : NAN;
 }
 
 // Python float() semantics on a stripped string; empty/invalid -> NaN
@@ -203,9 +248,7 @@ class Parser {
             const char* v1 = (const char*)memchr(p_, q, (size_t)(e_ - p_));
             if (!v1) { err_ = true; return false; }
             p_ = v1 + 1;
-            std::string val;
-            decode(v0, v1, val);
-            t.attrs.emplace_back(local_name(a0, a1), std::move(val));
+            t.attrs.emplace_back(local_name(a0, a1), SV{v0, (size_t)(v1 - v0)});
         }
     }
     const char* p_;
@@ -217,23 +260,33 @@ int parse(const char* buf, size_t len, ShdGraphml& g) {
     Parser ps(buf, len);
     Tag tag;
     const char *t0, *t1;
-    std::unordered_map<std::string, Key> keys;
-    std::unordered_map<std::string, int32_t> idIndex;
-    std::vector<std::string> stack;
+    std::deque<std::pair<std::string, Key>> keys;           // stable addresses
+    std::unordered_map<std::string_view, int32_t> idIndex;  // views into buf or `arena`
+    std::deque<std::string> arena;                           // decoded ids with entities
+    std::vector<SV> stack;
     Key* curKey = nullptr;             // inside <key> (for <default>)
+    const Key* dataKey = nullptr;      // key of the open <data>
     bool inGraph = false, graphDone = false, keyNodeLoss = false;
     int ctx = 0;                       // 0 none, 1 graph, 2 node, 3 edge (current owner of <data>)
     int dataDepth = -1;                // stack depth of an open <data>/<default>
-    std::string text, dataKey;
+    // text of the open <data>/<default>: a view while it is one entity-free
+    // chunk (the common case), materialised otherwise
+    int textMode = 0;                  // 0 empty, 1 view, 2 string
+    SV textView;
+    std::string text;
     bool inDefault = false;
-    // per-owner attribute values by attribute name (latest wins, like a dict)
     double eLat = NAN, eLoss = NAN, vLoss = NAN;
     std::string gPdp;
     bool gPdpSet = false;
-    std::string eSrc, eDst;
+    SV eSrc, eDst;
+    std::string eSrcS, eDstS;          // decoded endpoints when they hold entities
     struct Pending { size_t edge; std::string src, dst; };
     std::vector<Pending> pending;
-    // defaults by kind, by name
+    auto find_key = [&](const SV& id) -> Key* {
+        for (auto& kv : keys)
+            if (kv.first.size() == id.n && memcmp(kv.first.data(), id.p, id.n) == 0) return &kv.second;
+        return nullptr;
+    };
     auto deflt = [&](const char* kind, const char* name, double& num, std::string* str,
                      bool* set) {
         for (auto& kv : keys) {
@@ -244,75 +297,129 @@ int parse(const char* buf, size_t len, ShdGraphml& g) {
             }
         }
     };
+    auto text_add = [&](const char* p0, const char* p1) {
+        if (p1 <= p0) return;
+        const SV c{p0, (size_t)(p1 - p0)};
+        if (textMode == 0 && !has_amp(c)) {
+            textView = c;
+            textMode = 1;
+            return;
+        }
+        if (textMode == 1) text.assign(textView.p, textView.n);
+        else if (textMode == 0) text.clear();
+        decode(p0, p1, text);
+        textMode = 2;
+    };
+    auto text_str = [&]() -> std::string {
+        return textMode == 1 ? std::string(textView.p, textView.n)
+                             : (textMode == 2 ? text : std::string());
+    };
+    auto text_num = [&]() -> double {
+        return textMode == 1 ? parse_num_view(textView) : (textMode == 2 ? parse_num(text) : NAN);
+    };
     double defLat = NAN, defLoss = NAN, defVLoss = NAN;   // fixed once <graph> opens
     auto finish_data = [&]() {
-        auto it = keys.find(dataKey);
-        if (it == keys.end()) return;
-        const Key& k = it->second;
+        if (!dataKey) return;
+        const Key& k = *dataKey;
         if (ctx == 1 && stack.size() == 2 && k.forKind == "graph" && k.name == "preferdirectpaths") {
-            gPdp = text;
+            gPdp = text_str();
             gPdpSet = true;
         } else if (ctx == 2) {
-            if (k.name == "packetloss") vLoss = parse_num(text);
+            if (k.name == "packetloss") vLoss = text_num();
         } else if (ctx == 3) {
-            if (k.name == "latency") eLat = parse_num(text);
-            else if (k.name == "packetloss") eLoss = parse_num(text);
+            if (k.name == "latency") eLat = text_num();
+            else if (k.name == "packetloss") eLoss = text_num();
         }
+    };
+    // an id as a lookup key: the raw view when entity-free, else decoded
+    auto id_view = [&](const SV* raw, std::string& scratch) -> std::string_view {
+        if (!raw) return std::string_view();
+        if (!has_amp(*raw)) return raw->view();
+        scratch.clear();
+        decode(raw->p, raw->p + raw->n, scratch);
+        return std::string_view(scratch);
     };
     for (;;) {
         const bool more = ps.next(tag, t0, t1);
-        if (dataDepth >= 0 && t1 > t0) decode(t0, t1, text);
+        if (dataDepth >= 0) text_add(t0, t1);
         if (!ps.cdata_.empty()) {
-            if (dataDepth >= 0) text += ps.cdata_;
+            if (dataDepth >= 0) {
+                if (textMode == 1) text.assign(textView.p, textView.n);
+                else if (textMode == 0) text.clear();
+                text += ps.cdata_;
+                textMode = 2;
+            }
             ps.cdata_.clear();
         }
         if (!more) break;
+        const SV nm = tag.name;
         if (!tag.end) {
-            const std::string& nm = tag.name;
-            if (nm == "key") {
+            if (nm.eq("key")) {
                 Key k;
-                if (auto v = tag.get("for")) k.forKind = *v;
-                if (auto v = tag.get("attr.name")) k.name = *v;
-                if (auto v = tag.get("attr.type")) k.type = *v;
-                const std::string id = tag.get("id") ? *tag.get("id") : std::string();
+                k.forKind = attr_str(tag, "for");
+                k.name = attr_str(tag, "attr.name");
+                k.type = attr_str(tag, "attr.type");
+                const std::string id = attr_str(tag, "id");
                 if (k.forKind == "node" && k.name == "packetloss") keyNodeLoss = true;
-                curKey = &(keys[id] = k);
-            } else if (nm == "default" && curKey) {
+                const SV idv{id.data(), id.size()};
+                Key* ex = find_key(idv);
+                if (ex) *ex = k;
+                else { keys.emplace_back(id, k); ex = &keys.back().second; }
+                curKey = ex;
+            } else if (nm.eq("default") && curKey) {
                 inDefault = true;
                 dataDepth = (int)stack.size();
-                text.clear();
-            } else if (nm == "graph" && !graphDone && !inGraph && stack.size() == 1) {
+                textMode = 0;
+            } else if (nm.eq("graph") && !graphDone && !inGraph && stack.size() == 1) {
                 inGraph = true;
                 ctx = 1;
-                const std::string* ed = tag.get("edgedefault");
-                g.directed = !ed || *ed == "directed";
+                const SV* ed = tag.raw("edgedefault");
+                g.directed = !ed || attr_str(tag, "edgedefault") == "directed";
                 deflt("graph", "preferdirectpaths", vLoss, &gPdp, &gPdpSet);
                 deflt("edge", "latency", defLat, nullptr, nullptr);
                 deflt("edge", "packetloss", defLoss, nullptr, nullptr);
                 deflt("node", "packetloss", defVLoss, nullptr, nullptr);
-            } else if (inGraph && nm == "node" && stack.size() == 2) {
+            } else if (inGraph && nm.eq("node") && stack.size() == 2) {
                 ctx = 2;
                 vLoss = defVLoss;
-                const std::string id = tag.get("id") ? *tag.get("id") : std::string();
-                if (!idIndex.emplace(id, (int32_t)g.ids.size()).second) return SHD_PE_EINVAL;
-                g.ids.push_back(id);
-            } else if (inGraph && nm == "edge" && stack.size() == 2) {
+                const SV* raw = tag.raw("id");
+                std::string_view key;
+                if (!raw) {
+                    key = std::string_view();
+                } else if (!has_amp(*raw)) {
+                    key = raw->view();
+                } else {
+                    arena.emplace_back();
+                    decode(raw->p, raw->p + raw->n, arena.back());
+                    key = arena.back();
+                }
+                if (!idIndex.emplace(key, (int32_t)g.ids.size()).second) return SHD_PE_EINVAL;
+                g.ids.emplace_back(key);
+            } else if (inGraph && nm.eq("edge") && stack.size() == 2) {
                 ctx = 3;
                 eLat = defLat;
                 eLoss = defLoss;
-                eSrc = tag.get("source") ? *tag.get("source") : std::string();
-                eDst = tag.get("target") ? *tag.get("target") : std::string();
-            } else if (inGraph && nm == "data" && ctx != 0) {
-                dataKey = tag.get("key") ? *tag.get("key") : std::string();
+                const SV* rs = tag.raw("source");
+                const SV* rd = tag.raw("target");
+                eSrc = rs ? *rs : SV{"", 0};
+                eDst = rd ? *rd : SV{"", 0};
+            } else if (inGraph && nm.eq("data") && ctx != 0) {
+                const SV* kr = tag.raw("key");
+                if (kr && has_amp(*kr)) {
+                    const std::string kd = attr_str(tag, "key");
+                    dataKey = find_key(SV{kd.data(), kd.size()});
+                } else {
+                    dataKey = kr ? find_key(*kr) : find_key(SV{"", 0});
+                }
                 dataDepth = (int)stack.size();
-                text.clear();
+                textMode = 0;
             }
             if (tag.selfClose) {
                 // an empty element: close it right away
-                if (nm == "data" && dataDepth == (int)stack.size()) {
+                if (nm.eq("data") && dataDepth == (int)stack.size()) {
                     finish_data();
                     dataDepth = -1;
-                } else if (nm == "default" && inDefault) {
+                } else if (nm.eq("default") && inDefault) {
                     curKey->deflt.clear();
                     curKey->hasDefault = false;    // ElementTree: text None -> no default
                     inDefault = false;
@@ -324,35 +431,35 @@ int parse(const char* buf, size_t len, ShdGraphml& g) {
                 continue;
             }
         } else {
-            if (stack.empty() || stack.back() != tag.name) return SHD_PE_EINVAL;
+            if (stack.empty() || !stack.back().eq(nm)) return SHD_PE_EINVAL;
             stack.pop_back();
         }
-        // ---- close of element `tag.name` at depth stack.size() ----
-        const std::string& nm = tag.name;
-        if (nm == "data" && dataDepth == (int)stack.size()) {
+        // ---- close of element `nm` at depth stack.size() ----
+        if (nm.eq("data") && dataDepth == (int)stack.size()) {
             finish_data();
             dataDepth = -1;
-        } else if (nm == "default" && inDefault) {
-            curKey->deflt = text;
-            curKey->hasDefault = !text.empty();       // ElementTree: no text -> None
+        } else if (nm.eq("default") && inDefault) {
+            curKey->deflt = text_str();
+            curKey->hasDefault = !curKey->deflt.empty();   // ElementTree: no text -> None
             inDefault = false;
             dataDepth = -1;
-        } else if (nm == "key") {
+        } else if (nm.eq("key")) {
             curKey = nullptr;
-        } else if (nm == "node" && ctx == 2 && stack.size() == 2) {
+        } else if (nm.eq("node") && ctx == 2 && stack.size() == 2) {
             g.vloss.push_back(vLoss);
             ctx = 1;
-        } else if (nm == "edge" && ctx == 3 && stack.size() == 2) {
+        } else if (nm.eq("edge") && ctx == 3 && stack.size() == 2) {
             // endpoints may name nodes declared later in the document
-            auto a = idIndex.find(eSrc), b = idIndex.find(eDst);
+            const std::string_view sv = id_view(&eSrc, eSrcS), dv = id_view(&eDst, eDstS);
+            auto a = idIndex.find(sv), b = idIndex.find(dv);
             if (a == idIndex.end() || b == idIndex.end())
-                pending.push_back({g.src.size(), eSrc, eDst});
+                pending.push_back({g.src.size(), std::string(sv), std::string(dv)});
             g.src.push_back(a == idIndex.end() ? -1 : a->second);
             g.dst.push_back(b == idIndex.end() ? -1 : b->second);
             g.lat.push_back(eLat);
             g.loss.push_back(eLoss);
             ctx = 1;
-        } else if (nm == "graph" && inGraph && stack.size() == 1) {
+        } else if (nm.eq("graph") && inGraph && stack.size() == 1) {
             inGraph = false;
             graphDone = true;
             ctx = 0;
