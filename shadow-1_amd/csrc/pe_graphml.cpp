@@ -18,7 +18,6 @@
 // entities and numeric character references, comments, processing
 // instructions, DOCTYPE, CDATA.  Namespace prefixes are ignored (GraphML's
 // default namespace is the common case).
-#include <cerrno>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -111,8 +110,10 @@ std::string attr_str(const Tag& t, const char* k) {
     return out;
 }
 
-// Python float() on the stripped text of a view that ends before a '<' (or
-// the buffer end); empty / invalid -> NaN.  strtod stops at the '<'.
+// Python float() on the stripped text of a view; empty / invalid -> NaN.
+// strtod runs on a NUL-terminated copy (it never reads past the view) in the
+// C locale Shadow runs in (a host that calls setlocale(LC_NUMERIC, ...) with
+// a decimal comma would need strtod_l).
 double parse_num_view(const SV& v) {
     size_t a = 0, b = v.n;
     while (a < b && is_space(v.p[a])) ++a;
@@ -135,22 +136,8 @@ double parse_num_view(const SV& v) {
     const double x = strtod(tmp, &end);
     return end == tmp + len ? x : NAN;
 }
+double parse_num(const std::string& s) { return parse_num_view(SV{s.data(), s.size()}); }
 
-// Python float() semantics on a stripped string; empty/invalid -> NaN
-double parse_num(const std::string& s) {
-    size_t a = 0, b = s.size();
-    while (a < b && is_space(s[a])) ++a;
-    while (b > a && is_space(s[b - 1])) --b;
-    if (a == b) return NAN;
-    const char* t = s.c_str() + a;            // NUL-terminated after the trailing blanks
-    const size_t len = b - a;
-    const size_t k = (t[0] == '-' || t[0] == '+') ? 1 : 0;
-    if (len > k + 1 && t[k] == '0' && (t[k + 1] == 'x' || t[k + 1] == 'X')) return NAN;   // no hex floats
-    char* end = nullptr;
-    const double v = strtod(t, &end);
-    if (end != t + len) return NAN;
-    return v;
-}
 
 }  // namespace
 
