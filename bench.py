@@ -66,7 +66,17 @@ def cpu_baseline(top, att, budget_s=12.0, max_rows=4000, threads=1):
         if time.perf_counter() - c0 < 0.25 * budget_s / 8:
             chunk = min(chunk * 2, 64 * threads)
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "source rows/s", "cores": threads, "kind": "port",
+    extra = {}
+    if threads == 1 and done:
+        # Dijkstra alone (no fold / row build), same rows: SURVEY.md §8(d)
+        # asks for the split; the fold + row is the difference
+        k, d0 = 0, time.perf_counter()
+        while k < done and time.perf_counter() - d0 < budget_s / 4:
+            og.raw(int(att[order[k]]), att)
+            k += 1
+        extra = {"dijkstra_only_rows_per_s": k / (time.perf_counter() - d0),
+                 "dijkstra_only_rows": k}
+    return {"value": done / dt, "unit": "source rows/s", "cores": threads, "kind": "port", **extra,
             "sample": f"{done} random source rows of the same workload (all {att.shape[0]} "
                       f"targets each), igraph-0.7.1-faithful 2-wheap Dijkstra + "
                       f"_topology_computePathProperties fold, {threads} thread(s), {dt:.1f} s"}

@@ -200,7 +200,8 @@ static void configure(ShdPe* pe) {
     BatchLaunch b{};
     b.lb = env_int("SHDPE_BATCH_LB", 16);
     if (b.lb != 8 && b.lb != 32) b.lb = 16;
-    b.threads = 1024;
+    b.threads = env_int("SHDPE_BATCH_THREADS", 1024);
+    if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     b.ldsBytes = batch_lds_bytes((int)n);
     int bPerCU = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bPerCU, batch_kernel_ptr(b.lb), b.threads,
