@@ -345,6 +345,28 @@ def test_batched_kernel(E, oracle_mod, case):
         assert st["rowsExact"] > 0
 
 
+def _chain(n, seed, vloss=False):
+    """Path graph 0-1-...-(n-1) with self-loops: one tree, depth up to n-1."""
+    rng = np.random.default_rng(seed)
+    src = np.concatenate([np.arange(n - 1), np.arange(n)])
+    dst = np.concatenate([np.arange(1, n), np.arange(n)])
+    m = src.shape[0]
+    return Topology(n, False, src, dst, rng.uniform(1.0, 50.0, m), rng.uniform(0.0, 0.02, m),
+                    rng.uniform(0.0, 0.01, n) if vloss else None)
+
+
+@pytest.mark.parametrize("n,vloss", [(4400, False), (300, True)])
+def test_batched_kernel_deep_trees(E, oracle_mod, n, vloss):
+    """Deep predecessor trees in k_batch_rows: many pointer-jumping rounds,
+    depth > LMAX (4096: Gauss-Seidel reliability sweeps) and, with vertex
+    loss, the chain fold of fold_rel_batch beyond 64 hops."""
+    top = _chain(n, seed=n, vloss=vloss)
+    att = np.arange(n, dtype=np.int32)
+    srcs = np.array([0, n - 1, n // 2, n // 3, 7], np.int32)
+    st = _check_engine(E, oracle_mod, top, att, sources=srcs, force=5)
+    assert st["mode"] == 1 and st["rowsExact"] == 0
+
+
 def test_native_graphml_to_engine(E, oracle_mod):
     """§8 f4 end to end: shipped GraphML -> shd_graphml_parse -> shd_pe_create
     (complete graph: direct rows), and the same file minus one edge (Dijkstra
