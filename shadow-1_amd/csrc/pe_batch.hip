@@ -234,13 +234,24 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             unsigned long long myMin = INF_BITS;
             int myAct = 0;
             const long long tg0 = dbg ? (long long)clock64() : 0;
+            // the queue entries of the group's NEXT vertices are loaded one
+            // iteration ahead (qn >= 1 here), so a vertex starts with its
+            // dist / row-range loads instead of a dependent queue round trip
+            int nq[BV];
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                const int idx = gid * BV + v;
+                nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
+            }
             for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
                 int u[BV], a0[BV], a1[BV];
                 unsigned long long db[BV], dub[BV];
 #pragma unroll
+                for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? nq[v] : -1;
+#pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    const int uq = ld_wg(&Q[i0 + v < qn ? i0 + v : i0]);
-                    u[v] = i0 + v < qn ? uq : -1;
+                    const int idx = i0 + NG * BV + v;
+                    nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
                 }
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
