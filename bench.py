@@ -1,21 +1,28 @@
 """Benchmark: path-table construction (source rows/sec), BASELINE.json metric.
 
-python bench.py --gpus N --steps K --warmup W [--workload c2] [--allgather]
+python bench.py --gpus N --steps K --warmup W [--workload c4] [--allgather]
 
 A step = one full path-table construction for the workload (all S source
-rows, S = T = attached vertices), sharded over the N ranks in contiguous
-blocks of rows (strong scaling: the table is fixed, ranks split it).  Each
-rank owns one engine on its own GPU (libshdpe.so, HIP kernels); no exchange
-on the data path.  --allgather additionally assembles the whole table on
-every rank with an RCCL all-gather over xGMI (reported separately).
+rows, S = T = attached vertices).  With N ranks (one process per GPU,
+torchrun) every rank builds ONE engine for its own GPU with
+shardIndex = rank, shardCount = N: the engine's shard plan
+(shd_pe_shard_bounds) gives it a contiguous block of rows with an equal
+number of kernel work units, and it computes only those (strong scaling: the
+table is fixed, ranks split it; no exchange on the data path).
+--allgather then assembles the whole table on every GPU through the
+engine-owned RCCL communicator (shd_pe_comm_init + shd_pe_gather, all
+fields), timed separately and never part of `value`.
 
-Inputs (graph, attached set) are uploaded before the timed region; rows stay
-in HBM (the D2H to the host path cache is outside `value`).
+Default workload: C4 (BASELINE.json configs[3], the north_star target:
+100k-vertex power-law topology, 16,384 attached sources).  Inputs (graph,
+attached set) are uploaded before the timed region; rows stay in HBM (the
+D2H to the host path cache is outside `value`).
 
 rank 0 prints ONE JSON line.  cpu_baseline = the oracle (C restatement of
 igraph 0.7.1 Dijkstra + topology.c fold) on 1 host thread, on a bounded
 sample of the same rows (the reference serialises all Dijkstra runs under
-graphLock, topology.c:1747-1781).
+graphLock, topology.c:1747-1781).  --tie-stress adds the 0.005-quantised
+variants (c2q, c4q: SURVEY.md §8d) with their tie-row counts.
 """
 import argparse
 import json
@@ -35,12 +42,6 @@ FP64_VALU_PEAK_TF = 78.6       # MI355X FP64 vector spec
 def algorithmic_bytes_per_row(n, m_arcs, T):
     """SURVEY.md §8(d) frozen formula for a sparse row: 12*m_arcs + 12*n + 20*T."""
     return 12 * m_arcs + 12 * n + 20 * T
-
-
-def shard(T, rank, world):
-    start = (T * rank) // world
-    end = (T * (rank + 1)) // world
-    return start, end - start
 
 
 def cpu_baseline(top, att, budget_s=12.0, max_rows=4000, threads=1):
@@ -95,7 +96,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--workload", default="c4")
     ap.add_argument("--allgather", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -104,6 +105,9 @@ def main():
                          "share is 16 CPUs, os.cpu_count() there shows the whole machine)")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the device-copy HBM bandwidth reference")
+    ap.add_argument("--tie-stress", default="c2q,c4q",
+                    help="comma list of quantised variants timed after the headline (rank 0, "
+                         "N=1; '' = off): their tie-row fraction and k_exact_rows time")
     ap.add_argument("--d2h-rows", type=int, default=2048,
                     help="rows copied to host buffers through shd_pe_get_row after the timed "
                          "region (PCIe-inclusive rate, reported separately; 0 = off)")
@@ -120,12 +124,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from shdpe import generators as G
-    from shdpe.engine import Engine
+    from shdpe.engine import Engine, DEBUG_ENV
 
+    # SHDPE_* tuning variables reach the library only through its debug flag
+    dbg = DEBUG_ENV if any(k.startswith("SHDPE_") for k in os.environ) else 0
     top, att = G.make_config(args.workload)
-    eng = Engine(top, att, device=local)
+    eng = Engine(top, att, device=local, shard_index=rank, shard_count=world, debug_flags=dbg)
     T = eng.T
-    start, count = shard(T, rank, world)
+    start, count = eng.owned
     st0 = eng.stats()
     n, m_arcs = st0["nVertices"], st0["nArcs"]
 
@@ -137,12 +143,12 @@ def main():
         eng.synchronize()
 
     for _ in range(args.warmup):
-        eng.compute_positions(start, count)
+        eng.compute_all()
     barrier_sync()
     eng.reset_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.compute_positions(start, count)
+        eng.compute_all()
     eng.synchronize()
     barrier_sync()
     elapsed = time.perf_counter() - t0
@@ -155,19 +161,19 @@ def main():
 
     gather = None
     if args.allgather and dist is not None:
-        import torch
-        # equal-size blocks for the collective (pad the last shard)
-        blk = (T + world - 1) // world
-        mine = torch.zeros(blk * T, dtype=torch.float64, device=f"cuda:{local}")
-        eng.copy_rows_device(start, count, d_lat=mine.data_ptr())
-        full = torch.empty(world * blk * T, dtype=torch.float64, device=f"cuda:{local}")
-        torch.cuda.synchronize(); dist.barrier()
+        # engine-owned RCCL communicator: rank 0 makes the id, torch hands it out
+        uid = [Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0])
+        barrier_sync()
         g0 = time.perf_counter()
-        dist.all_gather_into_tensor(full, mine)
-        torch.cuda.synchronize()
+        eng.gather()
+        barrier_sync()
         g1 = time.perf_counter()
-        gather = {"bytes_per_rank": mine.numel() * 8, "ms": (g1 - g0) * 1e3,
-                  "field": "latency f64"}
+        row_bytes = T * (8 + 8 + 4 + 1 + (4 if eng.store_pred else 0))
+        gather = {"ms": (g1 - g0) * 1e3, "bytes_received_per_rank": (T - count) * row_bytes,
+                  "fields": "lat f64, rel f64, hops i32, flags u8" + (", pred i32" if eng.store_pred else ""),
+                  "how": "shd_pe_gather: RCCL broadcast group (per-shard blocks) over xGMI"}
 
     d2h = None
     if args.d2h_rows > 0 and count > 0:
@@ -220,7 +226,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": args.workload, "vertices": n, "arcs": m_arcs,
+        "config": {"workload": args.workload, "desc": G.CONFIGS.get(args.workload, {}).get("desc"),
+                   "vertices": n, "arcs": m_arcs,
                    "sources": T, "targets": T, "rows_per_step": T,
                    "parallelism": f"source-row shards x{world}"},
         "edges_relaxed_per_s": m_arcs * rows_total / elapsed,
@@ -230,6 +237,7 @@ def main():
                      "algorithmic_per_launch": bytes_per_launch,
                      "avg_launch_ms": avg_launch_ms, "launches": launches},
         "rows_exact": st["rowsExact"] // max(1, args.steps),
+        "tie_row_fraction": st["rowsExact"] / max(1, args.steps * count),
         "ms_exact_per_step": st["msExactKernel"] / max(1, args.steps),
     }
     if rank == 0 and not args.no_stream:
@@ -249,11 +257,37 @@ def main():
             out["cpu_baseline_all_cores"] = allc
             out["speedup_vs_cpu_all_cores"] = value / allc["value"]
     eng.close()
+    if rank == 0 and world == 1 and args.tie_stress:
+        out["tie_stress"] = [tie_stress(wl, args.steps, dbg) for wl in args.tie_stress.split(",") if wl]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def tie_stress(workload, steps, dbg):
+    """Quantised variant (latencies rounded to 0.005 ms, like the shipped data):
+    rows whose equal-distance predecessor ties go to k_exact_rows."""
+    from shdpe import generators as G
+    from shdpe.engine import Engine
+    top, att = G.make_config(workload)
+    eng = Engine(top, att, debug_flags=dbg)
+    eng.compute_all()                        # warm-up
+    eng.reset_stats()
+    t0 = time.perf_counter()
+    k = max(1, min(steps, 2))
+    for _ in range(k):
+        eng.compute_all()
+    eng.synchronize()
+    el = (time.perf_counter() - t0) / k
+    st = eng.stats()
+    eng.close()
+    return {"workload": workload, "rows": int(eng.T), "ms_per_step": el * 1e3,
+            "rows_per_s": eng.T / el, "tie_rows": st["rowsExact"] // k,
+            "tie_row_fraction": st["rowsExact"] / k / eng.T,
+            "ms_exact_kernel_per_step": st["msExactKernel"] / k,
+            "ms_main_kernel_per_step": (st["msSparseKernel"] + st["msDenseKernel"]) / k}
 
 
 if __name__ == "__main__":

@@ -15,10 +15,17 @@
  * owns its device memory and stream; nothing it returns outlives
  * shd_pe_destroy().  The engine never calls back into topology.c.
  *
- * Threading: shd_pe_create/compute_* must be serialised by the caller (the
+ * Threading: compute / gather calls serialise on an engine mutex (the
  * reference holds graphLock around the igraph call, topology.c:1747-1781);
- * after a row is computed, shd_pe_get_row on it is read-only and may be called
- * concurrently.
+ * shd_pe_get_row / get_rows may be called from any number of threads at any
+ * time (a row not yet computed is computed under that mutex first; the
+ * computed-row flags are acquire/release atomics).
+ *
+ * Multi-GPU: the T table rows are split into G contiguous
+ * row shards.  One engine owns nDevices of them (one per device, computed
+ * concurrently); with shardCount > 1 several engines -- one per process --
+ * own the rest.  shd_pe_gather assembles the whole table on every device
+ * with RCCL over xGMI (shd_pe_comm_init joins the processes).
  */
 #ifndef SHD_PATHENGINE_H
 #define SHD_PATHENGINE_H
@@ -29,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SHD_PE_ABI_VERSION 1
+#define SHD_PE_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------ */
 #define SHD_PE_OK            0
@@ -42,6 +49,10 @@ extern "C" {
 #define SHD_PE_EHIP         -7   /* HIP runtime error during compute               */
 #define SHD_PE_ENOTATTACHED -8   /* vertex is not in the attached set              */
 #define SHD_PE_ENOEDGE      -9   /* direct path requested but (s,t) has no edge    */
+#define SHD_PE_ENOTOWNED   -10   /* row lives in another engine's shard (gather)   */
+#define SHD_PE_ETOOBIG     -11   /* graph exceeds the LDS-resident frontier limit
+                                    (about 520,000 vertices)                       */
+#define SHD_PE_ECOMM       -12   /* RCCL communicator missing or failed            */
 
 /* ---- per-entry flags (uint8) ------------------------------------------ */
 #define SHD_PE_F_UNREACHABLE 0x01u /* igraph could not reach t: not stored         */
@@ -71,15 +82,25 @@ typedef struct ShdPeGraphDesc {
 } ShdPeGraphDesc;
 
 /* ---- engine options ---------------------------------------------------- */
+#define SHD_PE_DEBUG_ENV      0x1  /* read SHDPE_* tuning variables (never in Shadow) */
+#define SHD_PE_DEBUG_COUNTERS 0x2  /* per-launch kernel counters on stderr          */
+
 typedef struct ShdPeOptions {
-    int32_t device;          /* HIP device ordinal (one engine per device)        */
-    int32_t batchRows;       /* source rows per launch; 0 = auto                  */
+    int32_t device;          /* first HIP device ordinal                          */
+    int32_t batchRows;       /* reserved, 0                                       */
     double delta;            /* delta-stepping bucket width (ms); 0 = auto        */
     int32_t storePred;       /* keep a predecessor-vertex column in the table      */
     int32_t forceMode;       /* 0 auto, 1 sparse delta-stepping, 2 direct gather,
                                 3 exact igraph-heap kernel for every row (tests),
                                 4 dense blocked min-plus,
                                 5 batched multi-source delta-stepping             */
+    int32_t nDevices;        /* row shards in this engine, one per device; 0 = 1 */
+    const int32_t* devices;  /* NULL: device, device+1, ...; else nDevices ordinals
+                                (a repeated ordinal = several logical shards on
+                                one device, e.g. to test sharding on one GPU)    */
+    int32_t shardIndex;      /* multi-process: this engine's index ...            */
+    int32_t shardCount;      /* ... among shardCount engines (0 or 1: all rows)   */
+    int32_t debugFlags;      /* SHD_PE_DEBUG_*                                    */
 } ShdPeOptions;
 
 typedef struct ShdPe ShdPe;
@@ -107,6 +128,8 @@ typedef struct ShdPeStats {
                                   sweeps (skipped K chunks excluded) + pred pass */
     int32_t batched;           /* mode 1 runs k_batch_rows (multi-source batches)  */
     int32_t batchLanes;        /* sources per batch (LB) when batched              */
+    int32_t nShards;           /* row shards (devices) in this engine              */
+    double msGather;           /* device time of shd_pe_gather                     */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */
@@ -132,7 +155,8 @@ int shd_pe_is_complete(const ShdPe* pe);
 int32_t shd_pe_num_attached(const ShdPe* pe);
 int shd_pe_attached(const ShdPe* pe, int32_t* outVertices);
 
-/* Compute all rows (eager batch, e.g. on the first cache miss). */
+/* Compute all rows this engine owns (eager batch, e.g. on the first cache
+ * miss); every local shard on its own device, concurrently. */
 int shd_pe_compute_all(ShdPe* pe);
 
 /* Compute rows for the given sources (vertex ids, must be attached). */
@@ -163,10 +187,35 @@ int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* lat, double
 
 /* Copy rows [start, start+count) (table positions) of the device table into
  * caller DEVICE buffers (e.g. an RCCL all-gather staging area).  Row-major,
- * T entries per row.  Any pointer may be NULL. */
+ * T entries per row.  Any pointer may be NULL.  Rows not yet computed are
+ * computed first (as shd_pe_get_rows); rows of another engine's shard need
+ * shd_pe_gather first (SHD_PE_ENOTOWNED). */
 int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count,
                             double* dLat, double* dRel, int32_t* dHops,
                             uint8_t* dFlags);
+
+/* ---- multi-GPU ----------------------------------------- */
+/* Global row shards G = shardCount * nDevices and their position bounds
+ * (G + 1 entries: shard g owns rows [bounds[g], bounds[g+1])). */
+int32_t shd_pe_num_shards(const ShdPe* pe);
+int shd_pe_shard_bounds(const ShdPe* pe, int32_t* bounds);
+/* The plan itself (host only, no GPU): G contiguous blocks of T rows with
+ * equal numbers of `unit`-row work units (16 = one k_batch_rows batch). */
+int shd_pe_plan_shards(int32_t T, int32_t G, int32_t unit, int32_t* bounds);
+/* Rows this engine owns (the union of its shards, contiguous). */
+int shd_pe_owned_range(const ShdPe* pe, int32_t* start, int32_t* count);
+/* Assemble the whole T x T table on every device of this engine (computing
+ * missing owned rows first): RCCL broadcasts (all-gather with per-shard
+ * blocks) over xGMI between distinct devices / processes, device copies
+ * between logical shards of one device.  Afterwards every row is readable
+ * here.  Multi-process engines need shd_pe_comm_init first. */
+int shd_pe_gather(ShdPe* pe);
+/* Cross-process RCCL communicator, one rank per engine (nDevices == 1,
+ * rank = shardIndex, nranks = shardCount): one process makes the id, the
+ * host's own channel (MPI, a socket, torch.distributed) hands its bytes to
+ * every process, each calls shd_pe_comm_init. */
+int shd_pe_comm_unique_id(void* out, int32_t bytes);   /* bytes >= 128 */
+int shd_pe_comm_init(ShdPe* pe, const void* uniqueId, int32_t bytes);
 
 /* Wait for outstanding device work of this engine. */
 int shd_pe_synchronize(ShdPe* pe);

@@ -73,6 +73,8 @@ def _load():
                "orc_topology_cache_size"):
         getattr(lib, fn).argtypes = [vp]
         getattr(lib, fn).restype = C.c_int64
+    lib.orc_selftest_vector_order.argtypes = [C.c_int64, C.c_int32, C.c_uint64]
+    lib.orc_selftest_vector_order.restype = C.c_int32
     return lib
 
 

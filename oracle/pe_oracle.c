@@ -77,6 +77,49 @@ static int orc_vector_order(const int32_t* v, const int32_t* v2, int64_t m,
     return 0;
 }
 
+/* The same permutation as orc_vector_order -- (v ascending, v2 ascending,
+ * edge id DESCENDING) -- by two counting sorts with sequential reads, for
+ * edge lists where the linked-list walk's random accesses dominate (the
+ * 2e8-edge C3 graphs).  orc_selftest_vector_order pins the equivalence. */
+static int orc_vector_order_counting(const int32_t* v, const int32_t* v2, int64_t m,
+                                     int32_t nodes, int64_t* res) {
+    int64_t* cnt = calloc((size_t)nodes + 1, sizeof(int64_t));
+    int64_t* tmp = malloc((size_t)(m > 0 ? m : 1) * sizeof(int64_t));
+    if (!cnt || !tmp) { free(cnt); free(tmp); return -1; }
+    for (int64_t i = 0; i < m; i++) cnt[v2[i] + 1]++;
+    for (int32_t k = 0; k < nodes; k++) cnt[k + 1] += cnt[k];
+    for (int64_t i = m - 1; i >= 0; i--) tmp[cnt[v2[i]]++] = i;   /* ids descending per bucket */
+    memset(cnt, 0, ((size_t)nodes + 1) * sizeof(int64_t));
+    for (int64_t i = 0; i < m; i++) cnt[v[i] + 1]++;
+    for (int32_t k = 0; k < nodes; k++) cnt[k + 1] += cnt[k];
+    for (int64_t i = 0; i < m; i++) { int64_t e = tmp[i]; res[cnt[v[e]]++] = e; }   /* stable */
+    free(cnt);
+    free(tmp);
+    return 0;
+}
+
+static int orc_order(const int32_t* v, const int32_t* v2, int64_t m, int32_t nodes, int64_t* res) {
+    return m < ((int64_t)1 << 22) ? orc_vector_order(v, v2, m, nodes, res)
+                                  : orc_vector_order_counting(v, v2, m, nodes, res);
+}
+
+int32_t orc_selftest_vector_order(int64_t m, int32_t nodes, uint64_t seed) {
+    int32_t* a = malloc((size_t)m * sizeof(int32_t));
+    int32_t* b = malloc((size_t)m * sizeof(int32_t));
+    int64_t* r1 = malloc((size_t)m * sizeof(int64_t));
+    int64_t* r2 = malloc((size_t)m * sizeof(int64_t));
+    int32_t ok = a && b && r1 && r2;
+    uint64_t x = seed | 1;
+    for (int64_t i = 0; ok && i < m; i++) {   /* xorshift; few nodes -> many parallel edges */
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17; a[i] = (int32_t)(x % (uint64_t)nodes);
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17; b[i] = (int32_t)(x % (uint64_t)nodes);
+    }
+    if (ok) ok = !orc_vector_order(a, b, m, nodes, r1) && !orc_vector_order_counting(a, b, m, nodes, r2);
+    for (int64_t i = 0; ok && i < m; i++) ok = r1[i] == r2[i];
+    free(a); free(b); free(r1); free(r2);
+    return ok;
+}
+
 void orc_graph_free(OrcGraph* g) {
     if (!g) return;
     free(g->from); free(g->to); free(g->lat); free(g->loss); free(g->vloss);
@@ -120,8 +163,8 @@ OrcGraph* orc_graph_new(int32_t n, int64_t m, int32_t directed,
         if (!g->vloss) { orc_graph_free(g); return NULL; }
         memcpy(g->vloss, vertexLoss, (size_t)n * sizeof(double));
     }
-    if (orc_vector_order(g->from, g->to, m, n, g->oi) ||
-        orc_vector_order(g->to, g->from, m, n, g->ii)) {
+    if (orc_order(g->from, g->to, m, n, g->oi) ||
+        orc_order(g->to, g->from, m, n, g->ii)) {
         orc_graph_free(g);
         return NULL;
     }
@@ -681,7 +724,10 @@ static int compute_source_paths(OrcTopology* t, int32_t s, int32_t d) {
         return 0;
     int allSuccess = 1;
     for (int32_t j = 0; j < t->nAttached; j++) {
-        if (t->rflags[j] & (ORC_F_UNREACHABLE | ORC_F_NOEDGE)) { allSuccess = 0; continue; }
+        /* nVertices == 0 (no igraph path): skipped, isAllSuccess untouched (:1815) */
+        if (t->rflags[j] & ORC_F_UNREACHABLE) continue;
+        /* _topology_computePathProperties failed: isAllSuccess = FALSE (:1857) */
+        if (t->rflags[j] & ORC_F_NOEDGE) { allSuccess = 0; continue; }
         store_path(t, 0, s, t->attached[j], t->rlat[j], t->rrel[j]);   /* :1855 */
     }
     return allSuccess;

@@ -124,6 +124,10 @@ int64_t orc_topology_rows_computed(const OrcTopology* t);
 int64_t orc_topology_self_paths_computed(const OrcTopology* t);
 int64_t orc_topology_cache_size(const OrcTopology* t);
 
+/* Test hook: igraph's two-pass vector_order vs the counting-sort form on a
+ * random multigraph edge list; 1 when identical. */
+int32_t orc_selftest_vector_order(int64_t m, int32_t nodes, uint64_t seed);
+
 #ifdef __cplusplus
 }
 #endif

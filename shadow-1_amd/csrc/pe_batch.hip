@@ -683,7 +683,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         // ================= 5. row writer (topology.c:1805-1864) ==============
         if (row >= 0 && !((ambMask >> l) & 1u)) {
             const int T = (int)tab.T;
-            const size_t base = (size_t)row * (size_t)tab.T;
+            const size_t base = (size_t)(row - tab.rowStart) * (size_t)tab.T;
             for (int j = gid; j < T; j += NG) {
                 const int t = g.attached[j];
                 double L = 0.0, Rl = 0.0;

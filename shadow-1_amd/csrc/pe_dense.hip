@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void k_dense_write(DevGraph g0, DevTable tab, 
         Rv = acc;
         if (L == 0.0) { L = 1.0; f |= F_ZEROLAT; }
     }
-    const size_t idx = (size_t)r * (size_t)tab.T + j;
+    const size_t idx = (size_t)(r - tab.rowStart) * (size_t)tab.T + j;
     dglobal(tab.lat)[idx] = L;
     dglobal(tab.rel)[idx] = Rv;
     dglobal(tab.hops)[idx] = h;
@@ -346,7 +346,7 @@ void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int
 int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, const double* Rl,
                       double* D, int32_t* P, uint8_t* rowActive, uint8_t* rowChanged,
                       uint8_t* rowAmb, int32_t* dAny, uint8_t* chunkEpoch, const int32_t* dRows,
-                      int32_t nRows, int64_t n, void* stream, int* sweepsOut,
+                      int32_t nRows, int64_t n, const Tuning& tu, void* stream, int* sweepsOut,
                       double* flopsOut) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t ldD = n;
@@ -355,17 +355,13 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
     (void)hipMemsetAsync(rowAmb, 0, nRows, st);
     const unsigned gx = (unsigned)((n + TCOL - 1) / TCOL);
     const dim3 gridS(gx, (unsigned)((nRows + 16 * MI_SWEEP - 1) / (16 * MI_SWEEP)));
-    static const int predMi = [] {
-        const char* e = std::getenv("SHDPE_PRED_MI");
-        return e && *e ? std::atoi(e) : MI_PRED;
-    }();
-    const int miP = predMi == 2 ? 2 : MI_PRED;
+    const int miP = tu.densePredMi == 2 ? 2 : MI_PRED;
     const dim3 gridP(gx, (unsigned)((nRows + 16 * miP - 1) / (16 * miP)));
     // chunk epochs (uint8): sweep t visits chunks changed at t-1 or t; the
     // initial rows count as changed at epoch 0.  Off beyond 250 sweeps or
     // when the chunk list would not fit.
     const int64_t nch = (n + KB - 1) / KB;
-    const bool epochs = nch <= MAXCH && !std::getenv("SHDPE_DENSE_NO_EPOCH");
+    const bool epochs = nch <= MAXCH && tu.denseEpochs;
     if (epochs)
         (void)hipMemsetAsync(chunkEpoch, 0, (size_t)gridS.y * (size_t)nch, st);
     int sweeps = 0;
@@ -385,7 +381,7 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
         std::memcpy(&vis, &cnt[2], 8);
         visits += (double)vis;
         std::swap(rowActive, rowChanged);
-        if (std::getenv("SHDPE_DEBUG")) {
+        if (tu.debug) {
             std::vector<uint8_t> h(nRows);
             (void)hipMemcpy(h.data(), rowActive, nRows, hipMemcpyDeviceToHost);
             long c = 0;

@@ -55,6 +55,9 @@ struct DevGraph {
     const uint32_t* heavyBits; // [ceil(n/32)] vertices with degree >= heavyDeg
 };
 
+// A table holds the contiguous block of rows [rowStart, rowStart + rows) of
+// the T x T path table (one device shard, or the whole table); kernels write
+// row position r at local row r - rowStart.
 struct DevTable {
     double* lat;
     double* rel;
@@ -62,6 +65,20 @@ struct DevTable {
     int32_t* pred;     // may be null
     uint8_t* flags;
     int64_t T;
+    int64_t rowStart;
+};
+
+// Engine tuning (defaults in the engine; SHDPE_* environment overrides only
+// with SHD_PE_DEBUG_ENV, never in a production build of Shadow).
+struct Tuning {
+    int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
+    double deltaFactor = 16.0;
+    int exactHc = 0, exactPerCU = 0, exactAos = 0;
+    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0;
+    double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
+    double denseMin = 0.25, denseBatchGB = 24.0;
+    int densePredMi = 2, denseEpochs = 1;
+    int debug = 0, streamWgPerCU = 4;
 };
 
 // k_exact_rows heap entry (igraph_2wheap_t data + index, labels alongside)
@@ -133,7 +150,7 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
                         const SparseLaunch& cfg, int32_t* dDbg, void* stream);
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
-                       bool ldsIndex, void* stream);
+                       bool ldsIndex, bool forceGlobalHeap, void* stream);
 void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
                         int32_t nRows, void* stream);
 int sparse_max_threads();
@@ -151,7 +168,7 @@ void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int
 int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, const double* Rl,
                       double* D, int32_t* P, uint8_t* rowActive, uint8_t* rowChanged,
                       uint8_t* rowAmb, int32_t* dAny, uint8_t* chunkEpoch, const int32_t* dRows,
-                      int32_t nRows, int64_t n, void* stream, int* sweepsOut,
+                      int32_t nRows, int64_t n, const Tuning& tu, void* stream, int* sweepsOut,
                       double* flopsOut);
 
 }  // namespace shdpe

@@ -4,15 +4,31 @@
 // per-target fold) with device kernels; see include/shd_pathengine.h.
 // No CPU compute fallback: every row comes from a gfx950 kernel, and create
 // fails with SHD_PE_ENODEV when no device is usable.
+//
+// Multi-GPU: the T table rows are split into G contiguous
+// row shards of (near-)equal kernel work units (shd_pe_plan_shards).  One
+// engine owns one or more of them, one per device (nDevices); several
+// engines in several processes own the rest (shardIndex / shardCount).  Each
+// shard holds its own graph copy, stream and a shard-sized table
+// (rows x T); compute runs all local shards concurrently (one host thread
+// per device), never exchanging data.  shd_pe_gather assembles the whole
+// table on every device with RCCL (a group of broadcasts = all-gather with
+// per-shard sizes) over xGMI, or with device copies when several logical
+// shards share a device.  The reference serialises every row on one core
+// under graphLock (topology.c:1747-1781).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "pe_device.hpp"
@@ -21,55 +37,70 @@
 
 using namespace shdpe;
 
-struct ShdPe {
-    HostGraph hg;
-    std::vector<int32_t> attached;   // unique, first-occurrence order
-    std::vector<int32_t> posOf;      // vertex -> table position or -1
-    ShdPeOptions opt{};
+namespace {
+
+constexpr int LDS_BYTES = 160 * 1024;
+
+struct Shard {
+    int gindex = 0;                 // global shard index
     int device = 0;
     int numCUs = 256;
+    int32_t rowStart = 0, rowCount = 0;   // table positions owned
     hipStream_t stream = nullptr;
-    hipStream_t copyStream = nullptr;     // D2H of rows (shd_pe_get_rows)
-    unsigned char* stage[2] = {nullptr, nullptr};   // pinned host staging
-    size_t stageBytes = 0;
-    std::mutex copyMu;
+    hipStream_t copyStream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evA = nullptr, evB = nullptr;
     std::vector<void*> allocs;
     DevGraph dg{};
-    DevTable tab{};
+    DevTable tab{};                 // this shard's rows
     DevScratch sc{};
     bool tableReady = false;
     int32_t* dRows = nullptr;
     uint8_t* dRowAmbig = nullptr;
-    int32_t* dDbg = nullptr;          // per-row kernel counters (SHDPE_DEBUG=1)
+    int32_t* dDbg = nullptr;
     int32_t rowsCap = 0;
     SparseLaunch cfg{};
-    int exactGrid = 0;
-    int exactHc = 1;
+    int exactGrid = 0, exactHc = 1;
     bool exactLdsIdx = false;
-    int mode = 1;
-    std::vector<uint8_t> rowDone;
-    // batched multi-source sparse path (pe_batch.hip)
-    bool batched = false;
     BatchLaunch bcfg{};
     BatchScratch bsc{};
     bool batchReady = false;
     int32_t* dBatchRows = nullptr;
     uint8_t* dBatchAmb = nullptr;
-    std::vector<int32_t> rank;        // table position -> BFS visit rank
-    // dense path (mode 3)
-    double* dW = nullptr;
-    double* dRl = nullptr;
-    double* dD = nullptr;
+    double *dW = nullptr, *dRl = nullptr, *dD = nullptr;
     int32_t* dP = nullptr;
-    uint8_t* dRowA = nullptr;
-    uint8_t* dRowB = nullptr;
-    uint8_t* dRowAmbD = nullptr;
-    uint8_t* dChunkEpoch = nullptr;   // dense: last sweep that changed (row tile, K chunk)
+    uint8_t *dRowA = nullptr, *dRowB = nullptr, *dRowAmbD = nullptr, *dChunkEpoch = nullptr;
     int32_t* dAny = nullptr;
     int32_t denseRows = 0;
+    DevTable full{};                // whole table on this device after gather
+    bool fullOwner = false;         // first shard on its device owns `full`
+    ncclComm_t comm = nullptr;      // in-process communicator (distinct devices)
     ShdPeStats stats{};
-    std::mutex mu;
+};
+
+}  // namespace
+
+struct ShdPe {
+    HostGraph hg;
+    std::vector<int32_t> attached;   // unique, first-occurrence order
+    std::vector<int32_t> posOf;      // vertex -> table position or -1
+    ShdPeOptions opt{};
+    Tuning tu{};
+    int mode = 1;
+    bool batched = false;
+    std::vector<int32_t> rank;       // table position -> BFS visit rank
+    int G = 1;                       // global row shards
+    std::vector<int32_t> bounds;     // G + 1 position bounds
+    int firstShard = 0;              // global index of shards[0]
+    std::vector<std::unique_ptr<Shard>> shards;
+    std::unique_ptr<std::atomic<uint8_t>[]> rowDone;
+    bool gathered = false;
+    ncclComm_t xcomm = nullptr;      // cross-process communicator (shd_pe_comm_init)
+    int32_t ownStart = 0, ownEnd = 0;
+    unsigned char* stage[2] = {nullptr, nullptr};   // pinned host staging (portable)
+    size_t stageBytes = 0;
+    std::mutex mu;                   // compute / gather
+    std::mutex copyMu;               // staging buffers
+    double msGather = 0.0;
 };
 
 #define HIPCHK(x)                                   \
@@ -77,40 +108,64 @@ struct ShdPe {
         if ((x) != hipSuccess) return SHD_PE_EHIP;  \
     } while (0)
 
-static int dev_alloc(ShdPe* pe, void** p, size_t bytes) {
+static int dev_alloc(Shard* s, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (hipMalloc(p, bytes) != hipSuccess) { *p = nullptr; return SHD_PE_ENOMEM; }
-    pe->allocs.push_back(*p);
+    s->allocs.push_back(*p);
     return SHD_PE_OK;
 }
 
-template <class T>
-static int dev_upload(ShdPe* pe, T** dst, const std::vector<T>& src) {
-    int rc = dev_alloc(pe, reinterpret_cast<void**>(dst), src.size() * sizeof(T));
+template <class T, class A>
+static int dev_upload(Shard* s, T** dst, const std::vector<T, A>& src) {
+    int rc = dev_alloc(s, reinterpret_cast<void**>(dst), src.size() * sizeof(T));
     if (rc) return rc;
     if (!src.empty())
         HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
     return SHD_PE_OK;
 }
 
-static double env_double(const char* name, double dflt) {
-    const char* v = std::getenv(name);
-    return (v && *v) ? std::atof(v) : dflt;
-}
-
-static int env_int(const char* name, int dflt) {
-    const char* v = std::getenv(name);
-    return (v && *v) ? std::atoi(v) : dflt;
+// SHDPE_* tuning variables are read only under SHD_PE_DEBUG_ENV: a library
+// linked into Shadow must not change behaviour with the environment.
+static void read_tuning(Tuning& t, int32_t flags) {
+    if (flags & SHD_PE_DEBUG_COUNTERS) t.debug = 1;
+    if (!(flags & SHD_PE_DEBUG_ENV)) return;
+    auto gi = [](const char* k, int& v) { const char* e = std::getenv(k); if (e && *e) v = std::atoi(e); };
+    auto gd = [](const char* k, double& v) { const char* e = std::getenv(k); if (e && *e) v = std::atof(e); };
+    gi("SHDPE_THREADS", t.spThreads);
+    gi("SHDPE_HEAVY_DEG", t.heavyDeg);
+    gi("SHDPE_LAYOUT", t.layout);
+    gi("SHDPE_WG_PER_CU", t.wgPerCU);
+    gi("SHDPE_KFLAGS", t.kflags);
+    gd("SHDPE_DELTA_FACTOR", t.deltaFactor);
+    gi("SHDPE_EXACT_HC", t.exactHc);
+    gi("SHDPE_EXACT_PER_CU", t.exactPerCU);
+    gi("SHDPE_EXACT_AOS", t.exactAos);
+    gi("SHDPE_BATCH", t.batch);
+    gi("SHDPE_BATCH_LB", t.batchLB);
+    gi("SHDPE_BATCH_THREADS", t.batchThreads);
+    gi("SHDPE_BATCH_GRID", t.batchGrid);
+    gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
+    gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
+    gd("SHDPE_DENSE_MIN", t.denseMin);
+    gd("SHDPE_DENSE_BATCH_GB", t.denseBatchGB);
+    gi("SHDPE_PRED_MI", t.densePredMi);
+    gi("SHDPE_DENSE_EPOCHS", t.denseEpochs);
+    gi("SHDPE_DEBUG", t.debug);
+    gi("SHDPE_STREAM_WG_PER_CU", t.streamWgPerCU);
 }
 
 extern "C" void shd_pe_default_options(ShdPeOptions* opt) {
     if (!opt) return;
     std::memset(opt, 0, sizeof(*opt));
     opt->device = 0;
-    opt->batchRows = 0;
     opt->delta = 0.0;
     opt->storePred = 1;
     opt->forceMode = 0;
+    opt->nDevices = 1;
+    opt->devices = nullptr;
+    opt->shardIndex = 0;
+    opt->shardCount = 1;
+    opt->debugFlags = 0;
 }
 
 extern "C" const char* shd_pe_strerror(int code) {
@@ -125,98 +180,107 @@ extern "C" const char* shd_pe_strerror(int code) {
         case SHD_PE_EHIP: return "HIP runtime error";
         case SHD_PE_ENOTATTACHED: return "vertex is not attached";
         case SHD_PE_ENOEDGE: return "no edge between the vertices";
+        case SHD_PE_ENOTOWNED: return "row belongs to another engine's shard (gather first)";
+        case SHD_PE_ETOOBIG: return "graph exceeds the engine's vertex limit";
+        case SHD_PE_ECOMM: return "RCCL communicator error";
         default: return "unknown error";
     }
 }
 
 static inline int a16(long x) { return (int)((x + 15) & ~15L); }
 
-static void configure(ShdPe* pe) {
+// Kernel configuration for one shard's device.  Returns SHD_PE_ETOOBIG when
+// no kernel layout can hold the graph's per-row LDS state.
+static int configure(ShdPe* pe, Shard* sh) {
     const HostGraph& g = pe->hg;
+    const Tuning& tu = pe->tu;
     const long n = g.n;
     const long nw = (n + 31) / 32;
-    const int LDS = 160 * 1024;
+    const int LDS = LDS_BYTES;
     SparseLaunch c{};
-    c.threads = env_int("SHDPE_THREADS", 512);
-    if (c.threads > sparse_max_threads()) c.threads = sparse_max_threads();
+    c.threads = std::min(tu.spThreads, sparse_max_threads());
     c.hcap = 256;
-    c.heavyDeg = env_int("SHDPE_HEAVY_DEG", 64);
+    c.heavyDeg = tu.heavyDeg;
     const int qmin = 2048;
     // LDS bytes per layout (queues are ping-pong pairs; LAYOUT 0/3 keep them in HBM)
     const int pend = a16(4 * nw), hbits = a16(4 * nw);
     const int hq2 = 2 * a16(4 * c.hcap);
-    const int need2 = 64 + pend + hbits + hq2 + a16(8 * n) + a16(2 * n) + a16(4 * (n + 1));
-    const int need1 = 64 + pend + hbits + hq2 + a16(8 * n);
-    const int need3 = 64 + pend + a16(8 * n);
-    const int need0 = 64 + pend + hbits;
-    int layout = 0, used = need0;
+    const long need2 = 64 + pend + hbits + hq2 + a16(8 * n) + a16(2 * n) + a16(4 * (n + 1));
+    const long need1 = 64 + pend + hbits + hq2 + a16(8 * n);
+    const long need3 = 64 + pend + a16(8 * n);
+    const long need0 = 64 + pend + hbits;
+    int layout = 0;
+    long used = need0;
     if (need2 + 8 * qmin <= LDS) { layout = 2; used = need2; }
     else if (need1 + 8 * qmin <= LDS) { layout = 1; used = need1; }
     // LAYOUT 3 keeps only dist + pending bits in LDS: ~1.4x slower per row
     // than LAYOUT 2 (measured, C2) but fits more rows per CU; take it when it
     // at least doubles the resident rows.
     const int maxWgByThreads = 2048 / std::max(c.threads, 64);
-    const int wg2 = layout == 2 ? std::min(maxWgByThreads, LDS / (need2 + 8 * qmin)) : 0;
-    const int wg3 = std::min(maxWgByThreads, LDS / need3);
-    if (need3 <= LDS && wg3 >= 2 * std::max(wg2, 1)) { layout = 3; used = need3; }
-    const int forced = env_int("SHDPE_LAYOUT", -1);
-    if (forced == 3 && need3 <= LDS) { layout = 3; used = need3; }
-    else if (forced == 2 && need2 + 8 * qmin <= LDS) { layout = 2; used = need2; }
-    else if (forced == 1 && need1 + 8 * qmin <= LDS) { layout = 1; used = need1; }
-    else if (forced == 0) { layout = 0; used = need0; }
+    const long wg2 = layout == 2 ? std::min<long>(maxWgByThreads, LDS / (need2 + 8 * qmin)) : 0;
+    const long wg3 = std::min<long>(maxWgByThreads, LDS / need3);
+    if (need3 <= LDS && wg3 >= 2 * std::max<long>(wg2, 1)) { layout = 3; used = need3; }
+    if (tu.layout == 3 && need3 <= LDS) { layout = 3; used = need3; }
+    else if (tu.layout == 2 && need2 + 8 * qmin <= LDS) { layout = 2; used = need2; }
+    else if (tu.layout == 1 && need1 + 8 * qmin <= LDS) { layout = 1; used = need1; }
+    else if (tu.layout == 0) { layout = 0; used = need0; }
     c.layout = layout;
     if (layout == 1 || layout == 2) {
         c.qcap = (int)std::min<long>((LDS - used) / 8, std::max<long>(n, 1024)) & ~3;
-        c.ldsBytes = used + 2 * a16(4 * c.qcap);
+        c.ldsBytes = (int)(used + 2 * a16(4 * c.qcap));
     } else {
         c.qcap = (int)((n + 63) & ~63L);
-        c.ldsBytes = used;
+        c.ldsBytes = (int)used;
     }
-    const int maxWG = env_int("SHDPE_WG_PER_CU", 8);
-    const int wgPerCU = std::max(1, std::min({maxWG, LDS / std::max(c.ldsBytes, 1),
-                                              2048 / c.threads}));
-    c.grid = pe->numCUs * wgPerCU;
-    const double factor = env_double("SHDPE_DELTA_FACTOR", 16.0);
-    c.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * factor;
+    const int wgPerCU = std::max(1, std::min<int>({tu.wgPerCU, LDS / std::max(c.ldsBytes, 1),
+                                                   2048 / c.threads}));
+    c.grid = sh->numCUs * wgPerCU;
+    c.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.deltaFactor;
     if (!(c.delta > 0)) c.delta = 1.0;
-    c.kflags = env_int("SHDPE_KFLAGS", 0);
-    pe->cfg = c;
+    c.kflags = tu.kflags;
+    sh->cfg = c;
     // k_exact_rows: index2 (4n) in LDS up to n = 24k, heap entries (24 B)
     // in LDS up to the budget, the tail of the heap in the global slot.  A
     // whole heap that fits leaves room for several rows per CU.
-    pe->exactLdsIdx = (size_t)4 * n <= 96 * 1024;
-    const long idxB = pe->exactLdsIdx ? 4 * n : 0;
+    sh->exactLdsIdx = (size_t)4 * n <= 96 * 1024;
+    const long idxB = sh->exactLdsIdx ? 4 * n : 0;
     const long perWG = std::min<long>(LDS, idxB + 24 * n + 16);
-    pe->exactHc = (int)std::max<long>(1, std::min<long>(n, (perWG - idxB - 16) / 24));
-    const int hcCap = env_int("SHDPE_EXACT_HC", 0);   // testing: force the global heap tail
-    if (hcCap > 0) pe->exactHc = std::min(pe->exactHc, hcCap);
+    sh->exactHc = (int)std::max<long>(1, std::min<long>(n, (perWG - idxB - 16) / 24));
+    if (tu.exactHc > 0) sh->exactHc = std::min(sh->exactHc, tu.exactHc);   // tests: global heap tail
     const int exPerCU = (int)std::max<long>(1, std::min<long>(8, LDS / perWG));
-    pe->exactGrid = pe->numCUs * env_int("SHDPE_EXACT_PER_CU", exPerCU);
-    pe->stats.deltaUsed = c.delta;
+    sh->exactGrid = sh->numCUs * (tu.exactPerCU > 0 ? tu.exactPerCU : exPerCU);
     // Batched multi-source kernel: the layout for graphs whose per-row state
-    // does not fit LDS (LAYOUT 0), or on request (SHDPE_BATCH=1 / forceMode 5).
-    const int wantBatch = env_int("SHDPE_BATCH", -1);
-    pe->batched = wantBatch == 1 || (wantBatch != 0 && layout == 0) || pe->opt.forceMode == 5;
+    // does not fit LDS (LAYOUT 0), or on request (forceMode 5).
+    pe->batched = pe->mode == 1 &&
+                  (tu.batch == 1 || (tu.batch != 0 && layout == 0) || pe->opt.forceMode == 5);
     BatchLaunch b{};
-    b.lb = env_int("SHDPE_BATCH_LB", 16);
-    if (b.lb != 8 && b.lb != 32) b.lb = 16;
-    b.threads = env_int("SHDPE_BATCH_THREADS", 1024);
+    // LB = 16 sources per batch; 8 when a shard has too few rows to give
+    // every CU a batch of 16 (8-GPU shards of C4)
+    b.lb = tu.batchLB;
+    if (b.lb != 8 && b.lb != 16 && b.lb != 32)
+        b.lb = ((int64_t)sh->rowCount + 15) / 16 < (int64_t)sh->numCUs ? 8 : 16;
+    b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     b.ldsBytes = batch_lds_bytes((int)n);
+    if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
+    if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
     int bPerCU = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bPerCU, batch_kernel_ptr(b.lb), b.threads,
-                                                     b.ldsBytes) != hipSuccess || bPerCU < 1)
+    if (b.ldsBytes <= LDS &&
+        (hipFuncSetAttribute(batch_kernel_ptr(b.lb), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             b.ldsBytes) != hipSuccess ||
+         hipOccupancyMaxActiveBlocksPerMultiprocessor(&bPerCU, batch_kernel_ptr(b.lb), b.threads,
+                                                      b.ldsBytes) != hipSuccess ||
+         bPerCU < 1))
         bPerCU = 1;
-    b.grid = pe->numCUs * bPerCU;
-    const int gcap = env_int("SHDPE_BATCH_GRID", 0);
-    if (gcap > 0 && gcap < b.grid) b.grid = gcap;
-    const double bf = env_double("SHDPE_BATCH_DELTA_FACTOR", 8.0);
-    b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * bf;
+    b.grid = sh->numCUs * bPerCU;
+    if (tu.batchGrid > 0 && tu.batchGrid < b.grid) b.grid = tu.batchGrid;
+    b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
     if (!(b.delta > 0)) b.delta = 1.0;
-    pe->bcfg = b;
-    if (pe->batched) pe->stats.deltaUsed = b.delta;
-    pe->stats.batched = pe->batched ? 1 : 0;
-    pe->stats.batchLanes = pe->batched ? b.lb : 0;
+    sh->bcfg = b;
+    sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
+    sh->stats.batched = pe->batched ? 1 : 0;
+    sh->stats.batchLanes = pe->batched ? b.lb : 0;
+    return SHD_PE_OK;
 }
 
 // BFS visit rank of every table position (components in vertex order):
@@ -251,47 +315,57 @@ static void compute_ranks(ShdPe* pe) {
         if (pe->posOf[v] >= 0) pe->rank[pe->posOf[v]] = k++;
 }
 
-extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attached,
-                             int32_t nAttached, const ShdPeOptions* opt, ShdPe** out) {
-    if (!out || !graph || nAttached <= 0 || !attached) return SHD_PE_EINVAL;
-    *out = nullptr;
-    ShdPe* pe = new (std::nothrow) ShdPe();
-    if (!pe) return SHD_PE_ENOMEM;
-    if (opt) pe->opt = *opt; else shd_pe_default_options(&pe->opt);
-    int rc = build_host_graph(graph, &pe->hg);
-    if (rc) { delete pe; return rc; }
+// Row-shard plan: G contiguous position ranges with equal numbers of kernel
+// work units (a unit = one batch of 16 rows in the batched sparse kernel,
+// one row otherwise).  Per-unit cost is near-uniform for this path: every
+// SSSP row settles all n vertices, every dense / direct row is n (T) wide
+// (measured per-batch cycle spread in DESIGN.md §6), so equal units are the
+// balanced split, and contiguous ranges let the all-gather land rows in
+// place.  Host-only (no device), exported for the CPU tests.
+extern "C" int shd_pe_plan_shards(int32_t T, int32_t G, int32_t unit, int32_t* bounds) {
+    if (T < 0 || G < 1 || unit < 1 || !bounds) return SHD_PE_EINVAL;
+    const int64_t units = ((int64_t)T + unit - 1) / unit;
+    for (int g = 0; g < G; ++g)
+        bounds[g] = (int32_t)std::min<int64_t>(T, (units * g / G) * unit);
+    bounds[G] = T;
+    return SHD_PE_OK;
+}
+
+static void plan_shards(ShdPe* pe) {
+    pe->bounds.assign(pe->G + 1, 0);
+    (void)shd_pe_plan_shards((int32_t)pe->attached.size(), pe->G, pe->batched ? 16 : 1,
+                             pe->bounds.data());
+}
+
+static void destroy_shard(Shard* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->comm) (void)ncclCommDestroy(s->comm);
+    for (void* p : s->allocs) (void)hipFree(p);
+    for (hipEvent_t e : {s->ev0, s->ev1, s->evA, s->evB})
+        if (e) (void)hipEventDestroy(e);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->copyStream) (void)hipStreamDestroy(s->copyStream);
+}
+
+// Device state of one shard: graph upload, stream, events, kernel config.
+static int init_shard(ShdPe* pe, Shard* sh) {
     const HostGraph& g = pe->hg;
-    pe->posOf.assign(g.n, -1);
-    for (int32_t i = 0; i < nAttached; ++i) {
-        const int32_t v = attached[i];
-        if (v < 0 || v >= g.n) { delete pe; return SHD_PE_EINVAL; }
-        if (pe->posOf[v] < 0) {
-            pe->posOf[v] = (int32_t)pe->attached.size();
-            pe->attached.push_back(v);
-        }
-    }
-    // ---- device ----
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || pe->opt.device < 0 ||
-        pe->opt.device >= ndev) {
-        delete pe;
-        return SHD_PE_ENODEV;
-    }
-    pe->device = pe->opt.device;
-    if (hipSetDevice(pe->device) != hipSuccess) { delete pe; return SHD_PE_ENODEV; }
+    if (hipSetDevice(sh->device) != hipSuccess) return SHD_PE_ENODEV;
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, pe->device) != hipSuccess) { delete pe; return SHD_PE_ENODEV; }
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) { delete pe; return SHD_PE_ENODEV; }
-    pe->numCUs = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&pe->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&pe->ev0) != hipSuccess || hipEventCreate(&pe->ev1) != hipSuccess ||
-        hipEventCreate(&pe->evA) != hipSuccess || hipEventCreate(&pe->evB) != hipSuccess) {
-        shd_pe_destroy(pe);
+    if (hipGetDeviceProperties(&prop, sh->device) != hipSuccess) return SHD_PE_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SHD_PE_ENODEV;
+    sh->numCUs = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&sh->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&sh->copyStream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&sh->ev0) != hipSuccess || hipEventCreate(&sh->ev1) != hipSuccess ||
+        hipEventCreate(&sh->evA) != hipSuccess || hipEventCreate(&sh->evB) != hipSuccess)
         return SHD_PE_ENODEV;
-    }
-    configure(pe);
+    int rc = configure(pe, sh);
+    if (rc) return rc;
     const int32_t T = (int32_t)pe->attached.size();
-    DevGraph& d = pe->dg;
+    DevGraph& d = sh->dg;
     d.n = g.n;
     d.T = T;
     std::vector<uint8_t> isAtt(g.n, 0);
@@ -299,20 +373,18 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
     int32_t *rowPtr, *col, *outToIn, *att;
     double *lat, *rel, *vrel, *sl, *sr;
     uint8_t *hs, *ia;
-    if ((rc = dev_upload(pe, &rowPtr, g.rowPtr)) || (rc = dev_upload(pe, &col, g.col)) ||
-        (rc = dev_upload(pe, &lat, g.lat)) || (rc = dev_upload(pe, &rel, g.rel)) ||
-        (rc = dev_upload(pe, &outToIn, g.outToIn)) || (rc = dev_upload(pe, &vrel, g.vrel)) ||
-        (rc = dev_upload(pe, &sl, g.selfLat)) || (rc = dev_upload(pe, &sr, g.selfRel)) ||
-        (rc = dev_upload(pe, &hs, g.hasSelf)) || (rc = dev_upload(pe, &att, pe->attached)) ||
-        (rc = dev_upload(pe, &ia, isAtt))) {
-        shd_pe_destroy(pe);
+    if ((rc = dev_upload(sh, &rowPtr, g.rowPtr)) || (rc = dev_upload(sh, &col, g.col)) ||
+        (rc = dev_upload(sh, &lat, g.lat)) || (rc = dev_upload(sh, &rel, g.rel)) ||
+        (rc = dev_upload(sh, &outToIn, g.outToIn)) || (rc = dev_upload(sh, &vrel, g.vrel)) ||
+        (rc = dev_upload(sh, &sl, g.selfLat)) || (rc = dev_upload(sh, &sr, g.selfRel)) ||
+        (rc = dev_upload(sh, &hs, g.hasSelf)) || (rc = dev_upload(sh, &att, pe->attached)) ||
+        (rc = dev_upload(sh, &ia, isAtt)))
         return rc;
-    }
     {
         std::vector<Arc> arcs(g.col.size());
         for (size_t a = 0; a < arcs.size(); ++a) arcs[a] = Arc{g.lat[a], g.col[a], 0};
         Arc* da;
-        if ((rc = dev_upload(pe, &da, arcs))) { shd_pe_destroy(pe); return rc; }
+        if ((rc = dev_upload(sh, &da, arcs))) return rc;
         d.arcs = da;
         std::vector<Arc3> a3(g.col.size());
         for (size_t a = 0; a < a3.size(); ++a) {
@@ -321,171 +393,240 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
             a3[a] = Arc3{g.col[a], (uint32_t)bits, (uint32_t)(bits >> 32)};
         }
         Arc3* d3;
-        if ((rc = dev_upload(pe, &d3, a3))) { shd_pe_destroy(pe); return rc; }
+        if ((rc = dev_upload(sh, &d3, a3))) return rc;
         d.arc3 = d3;
     }
     d.rowPtr = rowPtr; d.col = col; d.lat = lat; d.rel = rel; d.outToIn = outToIn;
     d.vrel = vrel; d.selfLat = sl; d.selfRel = sr; d.hasSelf = hs; d.attached = att;
     d.isAttached = ia;
     {
-        const int hd = pe->cfg.heavyDeg;
+        const int hd = sh->cfg.heavyDeg;
         std::vector<uint32_t> hb((g.n + 31) / 32, 0u);
         for (int32_t v = 0; v < g.n; ++v)
             if (g.rowPtr[v + 1] - g.rowPtr[v] >= hd) hb[v >> 5] |= 1u << (v & 31);
         uint32_t* dhb;
-        if ((rc = dev_upload(pe, &dhb, hb))) { shd_pe_destroy(pe); return rc; }
+        if ((rc = dev_upload(sh, &dhb, hb))) return rc;
         d.heavyBits = dhb;
     }
     if (g.directed) {
         int32_t *ip, *ic;
         double *il, *ir;
-        if ((rc = dev_upload(pe, &ip, g.inPtr)) || (rc = dev_upload(pe, &ic, g.inCol)) ||
-            (rc = dev_upload(pe, &il, g.inLat)) || (rc = dev_upload(pe, &ir, g.inRel))) {
-            shd_pe_destroy(pe);
+        if ((rc = dev_upload(sh, &ip, g.inPtr)) || (rc = dev_upload(sh, &ic, g.inCol)) ||
+            (rc = dev_upload(sh, &il, g.inLat)) || (rc = dev_upload(sh, &ir, g.inRel)))
             return rc;
-        }
         d.inPtr = ip; d.inCol = ic; d.inLat = il; d.inRel = ir;
     } else {
         d.inPtr = rowPtr; d.inCol = col; d.inLat = lat; d.inRel = rel;
     }
-    pe->mode = (g.isComplete && pe->opt.forceMode != 1 && pe->opt.forceMode != 3) ? 2 : 1;
-    if (pe->opt.forceMode == 2) pe->mode = 2;
-    {
-        // dense non-complete graphs: blocked min-plus (K2)
-        const double density = (double)g.nArcs() / ((double)g.n * (double)g.n);
-        const double dmin = env_double("SHDPE_DENSE_MIN", 0.25);
-        const bool fitsDense = (int64_t)g.n <= 65536;
-        if (pe->mode == 1 && pe->opt.forceMode == 0 && fitsDense && density >= dmin) pe->mode = 3;
-        if (pe->opt.forceMode == 4 && fitsDense) pe->mode = 3;
-    }
-    pe->rowDone.assign(T, 0);
-    if (pe->opt.forceMode == 5) pe->mode = 1;
-    if (pe->mode == 1 && pe->batched) compute_ranks(pe);
-    pe->stats.mode = pe->mode;
-    pe->stats.isComplete = g.isComplete ? 1 : 0;
-    pe->stats.nVertices = g.n;
-    pe->stats.nArcs = g.nArcs();
-    pe->stats.nAttached = T;
-    *out = pe;
+    sh->stats.mode = pe->mode;
+    sh->stats.isComplete = g.isComplete ? 1 : 0;
+    sh->stats.nVertices = g.n;
+    sh->stats.nArcs = g.nArcs();
+    sh->stats.nAttached = T;
     return SHD_PE_OK;
 }
 
-static int ensure_table(ShdPe* pe) {
-    if (pe->tableReady) return SHD_PE_OK;
+static int select_mode(ShdPe* pe) {
+    const HostGraph& g = pe->hg;
+    int mode = (g.isComplete && pe->opt.forceMode != 1 && pe->opt.forceMode != 3) ? 2 : 1;
+    if (pe->opt.forceMode == 2) mode = 2;
+    // dense non-complete graphs: blocked min-plus (K2)
+    const double density = (double)g.nArcs() / ((double)g.n * (double)g.n);
+    const bool fitsDense = (int64_t)g.n <= 65536;
+    if (mode == 1 && pe->opt.forceMode == 0 && fitsDense && density >= pe->tu.denseMin) mode = 3;
+    if (pe->opt.forceMode == 4 && fitsDense) mode = 3;
+    if (pe->opt.forceMode == 5) mode = 1;
+    return mode;
+}
+
+extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attached,
+                             int32_t nAttached, const ShdPeOptions* opt, ShdPe** out) {
+    if (!out || !graph || nAttached <= 0 || !attached) return SHD_PE_EINVAL;
+    *out = nullptr;
+    std::unique_ptr<ShdPe> pe(new (std::nothrow) ShdPe());
+    if (!pe) return SHD_PE_ENOMEM;
+    if (opt) pe->opt = *opt; else shd_pe_default_options(&pe->opt);
+    ShdPeOptions& o = pe->opt;
+    if (o.nDevices <= 0) o.nDevices = 1;
+    if (o.shardCount <= 0) o.shardCount = 1;
+    if (o.shardIndex < 0 || o.shardIndex >= o.shardCount || o.nDevices > 64) return SHD_PE_EINVAL;
+    read_tuning(pe->tu, o.debugFlags);
+    int rc = build_host_graph(graph, &pe->hg);
+    if (rc) return rc;
+    const HostGraph& g = pe->hg;
+    pe->posOf.assign(g.n, -1);
+    for (int32_t i = 0; i < nAttached; ++i) {
+        const int32_t v = attached[i];
+        if (v < 0 || v >= g.n) return SHD_PE_EINVAL;
+        if (pe->posOf[v] < 0) {
+            pe->posOf[v] = (int32_t)pe->attached.size();
+            pe->attached.push_back(v);
+        }
+    }
+    const int32_t T = (int32_t)pe->attached.size();
+    // ---- devices ----
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SHD_PE_ENODEV;
+    std::vector<int> devs(o.nDevices);
+    for (int i = 0; i < o.nDevices; ++i) {
+        devs[i] = o.devices ? o.devices[i] : o.device + i;
+        if (devs[i] < 0 || devs[i] >= ndev) return SHD_PE_ENODEV;
+    }
+    pe->mode = select_mode(pe.get());
+    pe->G = o.shardCount * o.nDevices;
+    pe->firstShard = o.shardIndex * o.nDevices;
+    // the batched-kernel decision (and so the shard unit) needs a configured
+    // shard: configure a probe on the first device with the whole table
+    {
+        Shard probe;
+        probe.device = devs[0];
+        if (hipSetDevice(probe.device) != hipSuccess) return SHD_PE_ENODEV;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, probe.device) != hipSuccess) return SHD_PE_ENODEV;
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SHD_PE_ENODEV;
+        probe.numCUs = prop.multiProcessorCount;
+        probe.rowCount = T;
+        if ((rc = configure(pe.get(), &probe))) return rc;
+    }
+    plan_shards(pe.get());
+    pe->ownStart = pe->bounds[pe->firstShard];
+    pe->ownEnd = pe->bounds[pe->firstShard + o.nDevices];
+    for (int i = 0; i < o.nDevices; ++i) {
+        std::unique_ptr<Shard> sh(new (std::nothrow) Shard());
+        if (!sh) return SHD_PE_ENOMEM;
+        sh->gindex = pe->firstShard + i;
+        sh->device = devs[i];
+        sh->rowStart = pe->bounds[sh->gindex];
+        sh->rowCount = pe->bounds[sh->gindex + 1] - sh->rowStart;
+        sh->fullOwner = std::find(devs.begin(), devs.begin() + i, devs[i]) == devs.begin() + i;
+        rc = init_shard(pe.get(), sh.get());
+        pe->shards.push_back(std::move(sh));
+        if (rc) { shd_pe_destroy(pe.release()); return rc; }
+    }
+    if (pe->mode == 1 && pe->batched) compute_ranks(pe.get());
+    pe->rowDone.reset(new (std::nothrow) std::atomic<uint8_t>[T]);
+    if (!pe->rowDone) { shd_pe_destroy(pe.release()); return SHD_PE_ENOMEM; }
+    for (int32_t i = 0; i < T; ++i) pe->rowDone[i].store(0, std::memory_order_relaxed);
+    *out = pe.release();
+    return SHD_PE_OK;
+}
+
+static int ensure_table(ShdPe* pe, Shard* sh) {
+    if (sh->tableReady) return SHD_PE_OK;
     const size_t T = pe->attached.size();
-    const size_t cells = T * T;
+    const size_t cells = (size_t)sh->rowCount * T;
     int rc;
     void *lat, *rel, *hops, *flags, *pred = nullptr;
-    if ((rc = dev_alloc(pe, &lat, cells * 8)) || (rc = dev_alloc(pe, &rel, cells * 8)) ||
-        (rc = dev_alloc(pe, &hops, cells * 4)) || (rc = dev_alloc(pe, &flags, cells)))
+    if ((rc = dev_alloc(sh, &lat, cells * 8)) || (rc = dev_alloc(sh, &rel, cells * 8)) ||
+        (rc = dev_alloc(sh, &hops, cells * 4)) || (rc = dev_alloc(sh, &flags, cells)))
         return rc;
-    if (pe->opt.storePred && (rc = dev_alloc(pe, &pred, cells * 4))) return rc;
-    pe->tab.lat = (double*)lat;
-    pe->tab.rel = (double*)rel;
-    pe->tab.hops = (int32_t*)hops;
-    pe->tab.flags = (uint8_t*)flags;
-    pe->tab.pred = (int32_t*)pred;
-    pe->tab.T = (int64_t)T;
+    if (pe->opt.storePred && (rc = dev_alloc(sh, &pred, cells * 4))) return rc;
+    sh->tab.lat = (double*)lat;
+    sh->tab.rel = (double*)rel;
+    sh->tab.hops = (int32_t*)hops;
+    sh->tab.flags = (uint8_t*)flags;
+    sh->tab.pred = (int32_t*)pred;
+    sh->tab.T = (int64_t)T;
+    sh->tab.rowStart = sh->rowStart;
     // scratch slots
-    const int slots = pe->batched ? pe->exactGrid : std::max(pe->cfg.grid, pe->exactGrid);
+    const int slots = pe->batched ? sh->exactGrid : std::max(sh->cfg.grid, sh->exactGrid);
     const size_t stride = ((size_t)pe->hg.n + 63) & ~(size_t)63;
-    const size_t heapStride = std::max<size_t>(1, (size_t)pe->hg.n - (size_t)pe->exactHc);
-    void *dist, *sh, *sr, *sp, *hk, *i2;
-    if ((rc = dev_alloc(pe, &dist, slots * stride * 8)) ||
-        (rc = dev_alloc(pe, &sh, slots * stride * 4)) ||
-        (rc = dev_alloc(pe, &sr, slots * stride * 8)) ||
-        (rc = dev_alloc(pe, &sp, slots * stride * 4)) ||
-        (rc = dev_alloc(pe, &hk, (size_t)pe->exactGrid * heapStride * sizeof(XEnt))) ||
-        (rc = dev_alloc(pe, &i2, pe->exactLdsIdx ? 16 : (size_t)pe->exactGrid * stride * 4)))
+    const size_t heapStride = std::max<size_t>(1, (size_t)pe->hg.n - (size_t)sh->exactHc);
+    void *dist, *sho, *sr, *sp, *hk, *i2;
+    if ((rc = dev_alloc(sh, &dist, slots * stride * 8)) ||
+        (rc = dev_alloc(sh, &sho, slots * stride * 4)) ||
+        (rc = dev_alloc(sh, &sr, slots * stride * 8)) ||
+        (rc = dev_alloc(sh, &sp, slots * stride * 4)) ||
+        (rc = dev_alloc(sh, &hk, (size_t)sh->exactGrid * heapStride * sizeof(XEnt))) ||
+        (rc = dev_alloc(sh, &i2, sh->exactLdsIdx ? 16 : (size_t)sh->exactGrid * stride * 4)))
         return rc;
-    pe->sc.dist = (double*)dist;
-    pe->sc.hops = (int32_t*)sh;
-    pe->sc.rel = (double*)sr;
-    pe->sc.pred = (int32_t*)sp;
-    pe->sc.heapEnt = (XEnt*)hk;
-    pe->sc.heapStride = (int64_t)heapStride;
-    pe->sc.index2 = (int32_t*)i2;
-    pe->sc.stride = (int64_t)stride;
-    if (!pe->batched && (pe->cfg.layout == 3 || pe->cfg.layout == 0)) {
+    sh->sc.dist = (double*)dist;
+    sh->sc.hops = (int32_t*)sho;
+    sh->sc.rel = (double*)sr;
+    sh->sc.pred = (int32_t*)sp;
+    sh->sc.heapEnt = (XEnt*)hk;
+    sh->sc.heapStride = (int64_t)heapStride;
+    sh->sc.index2 = (int32_t*)i2;
+    sh->sc.stride = (int64_t)stride;
+    if (!pe->batched && (sh->cfg.layout == 3 || sh->cfg.layout == 0)) {
         void* q;
-        const size_t per = 2 * ((size_t)pe->cfg.qcap + pe->cfg.hcap);
-        if ((rc = dev_alloc(pe, &q, (size_t)pe->cfg.grid * per * 4))) return rc;
-        pe->sc.queue = (int32_t*)q;
+        const size_t per = 2 * ((size_t)sh->cfg.qcap + sh->cfg.hcap);
+        if ((rc = dev_alloc(sh, &q, (size_t)sh->cfg.grid * per * 4))) return rc;
+        sh->sc.queue = (int32_t*)q;
     }
-    pe->rowsCap = (int32_t)std::min<size_t>(T, 1 << 20);
+    sh->rowsCap = (int32_t)std::max<size_t>(1, std::min<size_t>(sh->rowCount, 1 << 20));
     void *rows, *amb;
-    if ((rc = dev_alloc(pe, &rows, (size_t)pe->rowsCap * 4)) ||
-        (rc = dev_alloc(pe, &amb, (size_t)pe->rowsCap)))
+    if ((rc = dev_alloc(sh, &rows, (size_t)sh->rowsCap * 4)) ||
+        (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap)))
         return rc;
-    pe->dRows = (int32_t*)rows;
-    pe->dRowAmbig = (uint8_t*)amb;
-    if (env_int("SHDPE_DEBUG", 0)) {
+    sh->dRows = (int32_t*)rows;
+    sh->dRowAmbig = (uint8_t*)amb;
+    if (pe->tu.debug) {
         void* dbg;
-        if ((rc = dev_alloc(pe, &dbg, (size_t)pe->rowsCap * 64))) return rc;
-        pe->dDbg = (int32_t*)dbg;
+        if ((rc = dev_alloc(sh, &dbg, (size_t)sh->rowsCap * 64))) return rc;
+        sh->dDbg = (int32_t*)dbg;
     }
-    pe->tableReady = true;
+    sh->tableReady = true;
     return SHD_PE_OK;
 }
 
-static int ensure_batch(ShdPe* pe) {
-    if (pe->batchReady) return SHD_PE_OK;
+static int ensure_batch(ShdPe* pe, Shard* sh) {
+    if (sh->batchReady) return SHD_PE_OK;
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
-    const size_t LB = (size_t)pe->bcfg.lb;
-    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4 * 3;
+    const size_t LB = (size_t)sh->bcfg.lb;
+    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4;
     // scratch budget (default 64 GiB): fewer resident batches on huge graphs
-    const double budget = env_double("SHDPE_BATCH_SCRATCH_GB", 64.0) * (double)(1ull << 30);
+    const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
-    const size_t nBatchesAll = (pe->attached.size() + LB - 1) / LB;
-    size_t slots = std::min<size_t>({(size_t)pe->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
-    pe->bcfg.grid = (int32_t)slots;
+    const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
+    size_t slots = std::min<size_t>({(size_t)sh->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
+    sh->bcfg.grid = (int32_t)slots;
     int rc;
-    void *D, *R, *H, *P, *X, *pm, *q, *rows, *amb;
-    if ((rc = dev_alloc(pe, &D, slots * NS * LB * 8)) || (rc = dev_alloc(pe, &R, slots * NS * LB * 8)) ||
-        (rc = dev_alloc(pe, &X, slots * NS * LB * 16)) ||
-        (rc = dev_alloc(pe, &H, slots * NS * LB * 4)) || (rc = dev_alloc(pe, &P, slots * NS * LB * 4)) ||
-        (rc = dev_alloc(pe, &pm, slots * NS * 2 * 4)) || (rc = dev_alloc(pe, &q, slots * NS * 4)) ||
-        (rc = dev_alloc(pe, &rows, ((size_t)pe->rowsCap + 64) * 4)) ||
-        (rc = dev_alloc(pe, &amb, (size_t)pe->rowsCap + 64)))
+    void *D, *R, *H, *P, *X, *q, *rows, *amb;
+    if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
+        (rc = dev_alloc(sh, &X, slots * NS * LB * 16)) ||
+        (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
+        (rc = dev_alloc(sh, &q, slots * NS * 4)) ||
+        (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
+        (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)))
         return rc;
-    pe->bsc.D = (unsigned long long*)D;
-    pe->bsc.R = (double*)R;
-    pe->bsc.H = (int32_t*)H;
-    pe->bsc.P = (int32_t*)P;
-    pe->bsc.X = (int32_t*)X;
-    pe->bsc.pm = (uint32_t*)pm;
-    pe->bsc.queue = (int32_t*)q;
-    pe->bsc.nStride = (int64_t)NS;
-    pe->dBatchRows = (int32_t*)rows;
-    pe->dBatchAmb = (uint8_t*)amb;
-    pe->batchReady = true;
+    sh->bsc.D = (unsigned long long*)D;
+    sh->bsc.R = (double*)R;
+    sh->bsc.H = (int32_t*)H;
+    sh->bsc.P = (int32_t*)P;
+    sh->bsc.X = (int32_t*)X;
+    sh->bsc.queue = (int32_t*)q;
+    sh->bsc.nStride = (int64_t)NS;
+    sh->dBatchRows = (int32_t*)rows;
+    sh->dBatchAmb = (uint8_t*)amb;
+    sh->batchReady = true;
     return SHD_PE_OK;
 }
 
-static int ensure_dense(ShdPe* pe) {
-    if (pe->dW) return SHD_PE_OK;
+static int ensure_dense(ShdPe* pe, Shard* sh) {
+    if (sh->dW) return SHD_PE_OK;
     const int64_t n = pe->hg.n;
-    const int64_t T = (int64_t)pe->attached.size();
+    const int64_t R = std::max<int32_t>(1, sh->rowCount);
     int rc;
     void *w, *rl, *d, *p, *ra, *rb, *am, *any, *ce;
     // rows per batch: D (f64) + P (i32) per row
-    const int64_t budget = (int64_t)env_double("SHDPE_DENSE_BATCH_GB", 24.0) * (1LL << 30);
+    const int64_t budget = (int64_t)(pe->tu.denseBatchGB * (double)(1LL << 30));
     int64_t rows = std::max<int64_t>(64, budget / (n * 12));
-    rows = std::min<int64_t>(rows, T);
-    if ((rc = dev_alloc(pe, &w, (size_t)(n * n * 8))) || (rc = dev_alloc(pe, &rl, (size_t)(n * n * 8))) ||
-        (rc = dev_alloc(pe, &d, (size_t)(rows * n * 8))) || (rc = dev_alloc(pe, &p, (size_t)(rows * n * 4))) ||
-        (rc = dev_alloc(pe, &ra, (size_t)rows)) || (rc = dev_alloc(pe, &rb, (size_t)rows)) ||
-        (rc = dev_alloc(pe, &am, (size_t)rows)) || (rc = dev_alloc(pe, &any, 16)) ||
-        (rc = dev_alloc(pe, &ce, (size_t)((rows / 16 + 1) * (n / 16 + 1)))))
+    rows = std::min<int64_t>(rows, R);
+    if ((rc = dev_alloc(sh, &w, (size_t)(n * n * 8))) || (rc = dev_alloc(sh, &rl, (size_t)(n * n * 8))) ||
+        (rc = dev_alloc(sh, &d, (size_t)(rows * n * 8))) || (rc = dev_alloc(sh, &p, (size_t)(rows * n * 4))) ||
+        (rc = dev_alloc(sh, &ra, (size_t)rows)) || (rc = dev_alloc(sh, &rb, (size_t)rows)) ||
+        (rc = dev_alloc(sh, &am, (size_t)rows)) || (rc = dev_alloc(sh, &any, 16)) ||
+        (rc = dev_alloc(sh, &ce, (size_t)((rows / 16 + 1) * (n / 16 + 1)))))
         return rc;
-    pe->dChunkEpoch = (uint8_t*)ce;
-    pe->dW = (double*)w; pe->dRl = (double*)rl; pe->dD = (double*)d; pe->dP = (int32_t*)p;
-    pe->dRowA = (uint8_t*)ra; pe->dRowB = (uint8_t*)rb; pe->dRowAmbD = (uint8_t*)am;
-    pe->dAny = (int32_t*)any;
-    pe->denseRows = (int32_t)rows;
-    launch_dense_build(pe->dg, pe->dW, pe->dRl, n, pe->hg.nArcs(), pe->stream);
+    sh->dChunkEpoch = (uint8_t*)ce;
+    sh->dW = (double*)w; sh->dRl = (double*)rl; sh->dD = (double*)d; sh->dP = (int32_t*)p;
+    sh->dRowA = (uint8_t*)ra; sh->dRowB = (uint8_t*)rb; sh->dRowAmbD = (uint8_t*)am;
+    sh->dAny = (int32_t*)any;
+    sh->denseRows = (int32_t)rows;
+    launch_dense_build(sh->dg, sh->dW, sh->dRl, n, pe->hg.nArcs(), sh->stream);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(pe->stream));
+    HIPCHK(hipStreamSynchronize(sh->stream));
     return SHD_PE_OK;
 }
 
@@ -495,184 +636,235 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
-// Compute the given table positions (chunked); caller holds pe->mu.
-static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count) {
+// Kernel counters of k_batch_rows (SHD_PE_DEBUG_COUNTERS): phase cycles,
+// re-visits, jump rounds, per-batch cost spread.
+static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t nB) {
+    double ph = 0, pr = 0, kc[5] = {0, 0, 0, 0, 0}, arcsP = 0, lanesP = 0, bmax = 0, bmean = 0, cand = 0;
+    long rnd = 0, dmax = 0, ambB = 0, rep = 0;
+    double tMin = 1e30, tMax = 0, tSum = 0, tSq = 0;
+    for (int32_t i = 0; i < nB; ++i) {
+        const int32_t* d = d0 + 16 * i;
+        ph += d[0]; rnd += d[1]; dmax = std::max<long>(dmax, d[2]);
+        ambB += d[3] != 0;
+        rep += d[15];
+        pr += d[4];
+        double tb = 0;
+        for (int k = 0; k < 3; ++k) { kc[k] += 1024.0 * d[5 + k]; tb += 1024.0 * d[5 + k]; }
+        kc[3] += 1024.0 * d[11]; tb += 1024.0 * d[11];
+        kc[4] += 1024.0 * d[8]; tb += 1024.0 * d[8];
+        tMin = std::min(tMin, tb); tMax = std::max(tMax, tb); tSum += tb; tSq += tb * tb;
+        arcsP += 16.0 * d[9];
+        bmax += 1024.0 * d[12]; bmean += 1024.0 * d[13]; cand += d[14];
+        lanesP += d[10];
+    }
+    const double mean = tSum / std::max(nB, 1);
+    const double sd = std::sqrt(std::max(0.0, tSq / std::max(nB, 1) - mean * mean));
+    std::fprintf(stderr, "[shdpe] shard %d batch relax Mcycles/batch: sum over phases of group-busy max=%.2f mean=%.2f | candidates/batch=%.0f\n",
+                 sh->gindex, bmax / nB / 1e6, bmean / nB / 1e6, cand / nB);
+    std::fprintf(stderr, "[shdpe] batch arc-visits/batch=%.0f (%.2f x nArcs) active lanes/proc=%.2f\n",
+                 arcsP / nB, arcsP / nB / (double)pe->hg.nArcs(), lanesP / std::max(pr, 1.0));
+    std::fprintf(stderr, "[shdpe] batch Mcycles/batch: relax=%.2f pred=%.2f depth=%.2f rel=%.2f write=%.2f | "
+                 "per-batch total min=%.2f mean=%.2f max=%.2f sd=%.2f\n", kc[0] / nB / 1e6, kc[1] / nB / 1e6,
+                 kc[2] / nB / 1e6, kc[3] / nB / 1e6, kc[4] / nB / 1e6, tMin / 1e6, mean / 1e6, tMax / 1e6, sd / 1e6);
+    std::fprintf(stderr, "[shdpe] batch LB=%d batches=%d grid=%d delta=%.3f | phases/batch=%.1f "
+                 "vertex-procs/batch=%.0f (%.2f per vertex) | jump rounds/batch=%.1f max depth=%ld amb batches=%ld repairs=%ld\n",
+                 sh->bcfg.lb, nB, sh->bcfg.grid, sh->bcfg.delta, ph / nB, pr / nB,
+                 pr / nB / pe->hg.n, (double)rnd / nB, dmax, ambB, rep);
+}
+
+static void print_sparse_debug(ShdPe* pe, Shard* sh, const int32_t* dbg, int32_t cnt) {
+    double ph = 0, cy[4] = {0, 0, 0, 0}, sub[4] = {0, 0, 0, 0};
+    int phMax = 0, jMax = 0, mis = 0, am = 0;
+    long jSum = 0;
+    for (int32_t i = 0; i < cnt; ++i) {
+        const int32_t* d = dbg + 16 * i;
+        ph += d[0]; phMax = std::max(phMax, d[0]);
+        jMax = std::max(jMax, d[1]); jSum += d[1];
+        mis += d[2] != 0; am += d[3] != 0;
+        for (int k = 0; k < 4; ++k) cy[k] += 16.0 * d[4 + k];
+        for (int k = 0; k < 4; ++k) sub[k] += 16.0 * d[8 + k];
+    }
+    std::fprintf(stderr,
+                 "[shdpe] shard %d sparse rows=%d phases mean=%.1f max=%d | mismatch rows=%d "
+                 "jacobi rounds sum=%ld max=%d | ambiguous rows=%d | delta=%.3f | "
+                 "kcycles/row scan=%.1f relax=%.1f final=%.1f write=%.1f | "
+                 "cyc/phase bits=%.0f resv=%.0f light=%.0f heavy=%.0f\n",
+                 sh->gindex, cnt, ph / cnt, phMax, mis, jSum, jMax, am, sh->cfg.delta,
+                 cy[0] / cnt / 1e3, cy[1] / cnt / 1e3, cy[2] / cnt / 1e3, cy[3] / cnt / 1e3,
+                 sub[0] / ph, sub[1] / ph, sub[2] / ph, sub[3] / ph);
+    (void)pe;
+}
+
+// Compute the given table positions (all owned by `sh`), chunked.
+static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count) {
     if (count <= 0) return SHD_PE_OK;
-    if (hipSetDevice(pe->device) != hipSuccess) return SHD_PE_EHIP;
-    int rc = ensure_table(pe);
+    if (hipSetDevice(sh->device) != hipSuccess) return SHD_PE_EHIP;
+    int rc = ensure_table(pe, sh);
     if (rc) return rc;
     std::vector<uint8_t> amb;
     std::vector<int32_t> exactRows;
-    HIPCHK(hipEventRecord(pe->ev0, pe->stream));
-    for (int32_t c0 = 0; c0 < count; c0 += pe->rowsCap) {
-        const int32_t cnt = std::min(pe->rowsCap, count - c0);
-        HIPCHK(hipMemcpyAsync(pe->dRows, pos + c0, (size_t)cnt * 4, hipMemcpyHostToDevice,
-                              pe->stream));
+    ShdPeStats& st = sh->stats;
+    HIPCHK(hipEventRecord(sh->ev0, sh->stream));
+    for (int32_t c0 = 0; c0 < count; c0 += sh->rowsCap) {
+        const int32_t cnt = std::min(sh->rowsCap, count - c0);
+        HIPCHK(hipMemcpyAsync(sh->dRows, pos + c0, (size_t)cnt * 4, hipMemcpyHostToDevice,
+                              sh->stream));
         exactRows.clear();
         if (pe->mode == 2) {
-            HIPCHK(hipEventRecord(pe->evA, pe->stream));
-            launch_direct_rows(pe->dg, pe->tab, pe->dRows, cnt, pe->stream);
+            HIPCHK(hipEventRecord(sh->evA, sh->stream));
+            launch_direct_rows(sh->dg, sh->tab, sh->dRows, cnt, sh->stream);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(pe->evB, pe->stream));
-            HIPCHK(hipEventSynchronize(pe->evB));
-            pe->stats.msDirectKernel += elapsed(pe->evA, pe->evB);
-            pe->stats.launchesDirect++;
+            HIPCHK(hipEventRecord(sh->evB, sh->stream));
+            HIPCHK(hipEventSynchronize(sh->evB));
+            st.msDirectKernel += elapsed(sh->evA, sh->evB);
+            st.launchesDirect++;
         } else if (pe->opt.forceMode == 3) {
             exactRows.assign(pos + c0, pos + c0 + cnt);
         } else if (pe->mode == 3) {
-            if ((rc = ensure_dense(pe))) return rc;
-            for (int32_t d0 = 0; d0 < cnt; d0 += pe->denseRows) {
-                const int32_t dc = std::min(pe->denseRows, cnt - d0);
-                HIPCHK(hipEventRecord(pe->evA, pe->stream));
+            if ((rc = ensure_dense(pe, sh))) return rc;
+            for (int32_t d0 = 0; d0 < cnt; d0 += sh->denseRows) {
+                const int32_t dc = std::min(sh->denseRows, cnt - d0);
+                HIPCHK(hipEventRecord(sh->evA, sh->stream));
                 int sweeps = 0;
                 double flops = 0.0;
-                if (launch_dense_rows(pe->dg, pe->tab, pe->dW, pe->dRl, pe->dD, pe->dP, pe->dRowA,
-                                      pe->dRowB, pe->dRowAmbD, pe->dAny, pe->dChunkEpoch,
-                                      pe->dRows + d0, dc,
-                                      pe->hg.n, pe->stream, &sweeps, &flops))
+                if (launch_dense_rows(sh->dg, sh->tab, sh->dW, sh->dRl, sh->dD, sh->dP, sh->dRowA,
+                                      sh->dRowB, sh->dRowAmbD, sh->dAny, sh->dChunkEpoch,
+                                      sh->dRows + d0, dc, pe->hg.n, pe->tu, sh->stream, &sweeps,
+                                      &flops))
                     return SHD_PE_EHIP;
                 HIPCHK(hipGetLastError());
-                HIPCHK(hipEventRecord(pe->evB, pe->stream));
+                HIPCHK(hipEventRecord(sh->evB, sh->stream));
                 amb.resize(dc);
-                HIPCHK(hipMemcpyAsync(amb.data(), pe->dRowAmbD, dc, hipMemcpyDeviceToHost,
-                                      pe->stream));
-                HIPCHK(hipStreamSynchronize(pe->stream));
-                pe->stats.msDenseKernel += elapsed(pe->evA, pe->evB);
-                pe->stats.launchesDense++;
-                pe->stats.denseSweeps += sweeps;
-                pe->stats.denseFlops += flops;
+                HIPCHK(hipMemcpyAsync(amb.data(), sh->dRowAmbD, dc, hipMemcpyDeviceToHost,
+                                      sh->stream));
+                HIPCHK(hipStreamSynchronize(sh->stream));
+                st.msDenseKernel += elapsed(sh->evA, sh->evB);
+                st.launchesDense++;
+                st.denseSweeps += sweeps;
+                st.denseFlops += flops;
                 for (int32_t i = 0; i < dc; ++i)
                     if (amb[i]) exactRows.push_back(pos[c0 + d0 + i]);
             }
         } else if (pe->batched) {
-            if ((rc = ensure_batch(pe))) return rc;
+            if ((rc = ensure_batch(pe, sh))) return rc;
             // batches of LB nearby sources (BFS rank order), -1 pads the last
-            const int LB = pe->bcfg.lb;
+            const int LB = sh->bcfg.lb;
             std::vector<int32_t> order(pos + c0, pos + c0 + cnt);
             std::stable_sort(order.begin(), order.end(),
                              [&](int32_t a, int32_t b) { return pe->rank[a] < pe->rank[b]; });
             const int32_t nB = (cnt + LB - 1) / LB;
             order.resize((size_t)nB * LB, -1);
-            HIPCHK(hipMemcpyAsync(pe->dBatchRows, order.data(), order.size() * 4,
-                                  hipMemcpyHostToDevice, pe->stream));
-            if (pe->dDbg) HIPCHK(hipMemsetAsync(pe->dDbg, 0, (size_t)nB * 64, pe->stream));
-            HIPCHK(hipEventRecord(pe->evA, pe->stream));
-            launch_batch_rows(pe->dg, pe->tab, pe->bsc, pe->dBatchRows, nB, pe->dBatchAmb, pe->bcfg,
-                              pe->dDbg, pe->stream);
+            HIPCHK(hipMemcpyAsync(sh->dBatchRows, order.data(), order.size() * 4,
+                                  hipMemcpyHostToDevice, sh->stream));
+            if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 64, sh->stream));
+            HIPCHK(hipEventRecord(sh->evA, sh->stream));
+            launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
+                              sh->dDbg, sh->stream);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(pe->evB, pe->stream));
+            HIPCHK(hipEventRecord(sh->evB, sh->stream));
             amb.resize(order.size());
-            HIPCHK(hipMemcpyAsync(amb.data(), pe->dBatchAmb, order.size(), hipMemcpyDeviceToHost,
-                                  pe->stream));
-            HIPCHK(hipStreamSynchronize(pe->stream));
-            pe->stats.msSparseKernel += elapsed(pe->evA, pe->evB);
-            pe->stats.launchesSparse++;
+            HIPCHK(hipMemcpyAsync(amb.data(), sh->dBatchAmb, order.size(), hipMemcpyDeviceToHost,
+                                  sh->stream));
+            HIPCHK(hipStreamSynchronize(sh->stream));
+            st.msSparseKernel += elapsed(sh->evA, sh->evB);
+            st.launchesSparse++;
             for (size_t i = 0; i < order.size(); ++i)
                 if (order[i] >= 0 && amb[i]) exactRows.push_back(order[i]);
-            if (pe->dDbg) {
+            if (sh->dDbg) {
                 std::vector<int32_t> dbg((size_t)nB * 16);
-                HIPCHK(hipMemcpy(dbg.data(), pe->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
-                double ph = 0, pr = 0, kc[5] = {0, 0, 0, 0, 0}, arcsP = 0, lanesP = 0, bmax = 0, bmean = 0, cand = 0;
-                long rnd = 0, dmax = 0, ambB = 0, rep = 0;
-                for (int32_t i = 0; i < nB; ++i) {
-                    const int32_t* d = dbg.data() + 16 * i;
-                    ph += d[0]; rnd += d[1]; dmax = std::max<long>(dmax, d[2]);
-                    ambB += d[3] != 0;
-                    rep += d[15];
-                    pr += d[4];
-                    for (int k = 0; k < 3; ++k) kc[k] += 1024.0 * d[5 + k];
-                    kc[3] += 1024.0 * d[11];
-                    kc[4] += 1024.0 * d[8];
-                    arcsP += 16.0 * d[9];
-                    bmax += 1024.0 * d[12]; bmean += 1024.0 * d[13]; cand += d[14];
-                    lanesP += d[10];
-                }
-                std::fprintf(stderr, "[shdpe] batch relax Mcycles/batch: sum over phases of group-busy max=%.2f mean=%.2f | candidates/batch=%.0f\n",
-                             bmax / nB / 1e6, bmean / nB / 1e6, cand / nB);
-                std::fprintf(stderr, "[shdpe] batch arc-visits/batch=%.0f (%.2f x nArcs) active lanes/proc=%.2f\n",
-                             arcsP / nB, arcsP / nB / (double)pe->hg.nArcs(), lanesP / std::max(pr, 1.0));
-                std::fprintf(stderr, "[shdpe] batch Mcycles/batch: relax=%.2f pred=%.2f "
-                             "depth=%.2f rel=%.2f write=%.2f\n", kc[0] / nB / 1e6, kc[1] / nB / 1e6,
-                             kc[2] / nB / 1e6, kc[3] / nB / 1e6, kc[4] / nB / 1e6);
-                std::fprintf(stderr, "[shdpe] batch LB=%d batches=%d grid=%d delta=%.3f | phases/batch=%.1f "
-                             "vertex-procs/batch=%.0f (%.2f per vertex) | jump rounds/batch=%.1f max depth=%ld amb batches=%ld repairs=%ld\n",
-                             LB, nB, pe->bcfg.grid, pe->bcfg.delta, ph / nB, pr / nB,
-                             pr / nB / pe->hg.n, (double)rnd / nB, dmax, ambB, rep);
+                HIPCHK(hipMemcpy(dbg.data(), sh->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
+                print_batch_debug(pe, sh, dbg.data(), nB);
             }
         } else {
-            HIPCHK(hipEventRecord(pe->evA, pe->stream));
-            launch_sparse_rows(pe->dg, pe->tab, pe->sc, pe->dRows, cnt, pe->dRowAmbig, pe->cfg,
-                               pe->dDbg, pe->stream);
+            HIPCHK(hipEventRecord(sh->evA, sh->stream));
+            launch_sparse_rows(sh->dg, sh->tab, sh->sc, sh->dRows, cnt, sh->dRowAmbig, sh->cfg,
+                               sh->dDbg, sh->stream);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(pe->evB, pe->stream));
+            HIPCHK(hipEventRecord(sh->evB, sh->stream));
             amb.resize(cnt);
-            HIPCHK(hipMemcpyAsync(amb.data(), pe->dRowAmbig, cnt, hipMemcpyDeviceToHost,
-                                  pe->stream));
-            HIPCHK(hipStreamSynchronize(pe->stream));
-            pe->stats.msSparseKernel += elapsed(pe->evA, pe->evB);
-            pe->stats.launchesSparse++;
+            HIPCHK(hipMemcpyAsync(amb.data(), sh->dRowAmbig, cnt, hipMemcpyDeviceToHost,
+                                  sh->stream));
+            HIPCHK(hipStreamSynchronize(sh->stream));
+            st.msSparseKernel += elapsed(sh->evA, sh->evB);
+            st.launchesSparse++;
             for (int32_t i = 0; i < cnt; ++i)
                 if (amb[i]) exactRows.push_back(pos[c0 + i]);
-            if (pe->dDbg) {
+            if (sh->dDbg) {
                 std::vector<int32_t> dbg((size_t)cnt * 16);
-                HIPCHK(hipMemcpy(dbg.data(), pe->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
-                double ph = 0, cy[4] = {0, 0, 0, 0}, sub[4] = {0, 0, 0, 0};
-                int phMax = 0, jMax = 0, mis = 0, am = 0; long jSum = 0;
-                for (int32_t i = 0; i < cnt; ++i) {
-                    const int32_t* d = dbg.data() + 16 * i;
-                    ph += d[0]; phMax = std::max(phMax, d[0]);
-                    jMax = std::max(jMax, d[1]); jSum += d[1];
-                    mis += d[2] != 0; am += d[3] != 0;
-                    for (int k = 0; k < 4; ++k) cy[k] += 16.0 * d[4 + k];
-                    for (int k = 0; k < 4; ++k) sub[k] += 16.0 * d[8 + k];
-                }
-                {
-                    double a0 = 0, a1 = 0, a2 = 0, calls = 0;
-                    for (int32_t i = 0; i < cnt; ++i) {
-                        a0 += 16.0 * dbg[16 * i + 12]; a1 += 16.0 * dbg[16 * i + 13];
-                        a2 += 16.0 * dbg[16 * i + 14]; calls += dbg[16 * i + 15];
-                    }
-                    std::fprintf(stderr, "[shdpe] group call (wave0): calls/row=%.1f cyc arcs=%.0f "
-                                 "reduce=%.0f label=%.0f\n", calls / cnt, a0 / calls, a1 / calls,
-                                 a2 / calls);
-                }
-                std::fprintf(stderr,
-                             "[shdpe] sparse rows=%d phases mean=%.1f max=%d | mismatch rows=%d "
-                             "jacobi rounds sum=%ld max=%d | ambiguous rows=%d | delta=%.3f | "
-                             "kcycles/row scan=%.1f relax=%.1f final=%.1f write=%.1f | "
-                             "cyc/phase bits=%.0f resv=%.0f light=%.0f heavy=%.0f\n",
-                             cnt, ph / cnt, phMax, mis, jSum, jMax, am, pe->cfg.delta,
-                             cy[0] / cnt / 1e3, cy[1] / cnt / 1e3, cy[2] / cnt / 1e3,
-                             cy[3] / cnt / 1e3, sub[0] / ph, sub[1] / ph, sub[2] / ph,
-                             sub[3] / ph);
+                HIPCHK(hipMemcpy(dbg.data(), sh->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
+                print_sparse_debug(pe, sh, dbg.data(), cnt);
             }
         }
         if (!exactRows.empty()) {
-            HIPCHK(hipMemcpyAsync(pe->dRows, exactRows.data(), exactRows.size() * 4,
-                                  hipMemcpyHostToDevice, pe->stream));
-            HIPCHK(hipEventRecord(pe->evA, pe->stream));
-            launch_exact_rows(pe->dg, pe->tab, pe->sc, pe->dRows, (int32_t)exactRows.size(),
-                              pe->exactGrid, pe->exactHc, pe->exactLdsIdx, pe->stream);
+            HIPCHK(hipMemcpyAsync(sh->dRows, exactRows.data(), exactRows.size() * 4,
+                                  hipMemcpyHostToDevice, sh->stream));
+            HIPCHK(hipEventRecord(sh->evA, sh->stream));
+            launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
+                              sh->exactGrid, sh->exactHc, sh->exactLdsIdx,
+                              pe->tu.exactHc > 0 || pe->tu.exactAos, sh->stream);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(pe->evB, pe->stream));
-            HIPCHK(hipEventSynchronize(pe->evB));
-            pe->stats.msExactKernel += elapsed(pe->evA, pe->evB);
-            pe->stats.launchesExact++;
-            pe->stats.rowsExact += (int64_t)exactRows.size();
+            HIPCHK(hipEventRecord(sh->evB, sh->stream));
+            HIPCHK(hipEventSynchronize(sh->evB));
+            st.msExactKernel += elapsed(sh->evA, sh->evB);
+            st.launchesExact++;
+            st.rowsExact += (int64_t)exactRows.size();
         }
     }
-    HIPCHK(hipEventRecord(pe->ev1, pe->stream));
-    HIPCHK(hipEventSynchronize(pe->ev1));
-    pe->stats.msTotal += elapsed(pe->ev0, pe->ev1);
-    pe->stats.rowsComputed += count;
-    pe->stats.arcsRelaxed += (int64_t)count * pe->hg.nArcs();
-    for (int32_t i = 0; i < count; ++i) pe->rowDone[pos[i]] = 1;
+    HIPCHK(hipEventRecord(sh->ev1, sh->stream));
+    HIPCHK(hipEventSynchronize(sh->ev1));
+    st.msTotal += elapsed(sh->ev0, sh->ev1);
+    st.rowsComputed += count;
+    st.arcsRelaxed += (int64_t)count * pe->hg.nArcs();
+    for (int32_t i = 0; i < count; ++i) pe->rowDone[pos[i]].store(1, std::memory_order_release);
     return SHD_PE_OK;
+}
+
+static Shard* owner_of(ShdPe* pe, int32_t p) {
+    for (auto& s : pe->shards)
+        if (p >= s->rowStart && p < s->rowStart + s->rowCount) return s.get();
+    return nullptr;
+}
+
+// Compute positions (caller holds pe->mu): split by shard, one host thread
+// per shard when several shards have work (their devices run concurrently).
+static int compute_positions_locked(ShdPe* pe, const int32_t* pos, int32_t count) {
+    if (count <= 0) return SHD_PE_OK;
+    std::vector<std::vector<int32_t>> per(pe->shards.size());
+    for (int32_t i = 0; i < count; ++i) {
+        Shard* s = owner_of(pe, pos[i]);
+        if (!s) return SHD_PE_ENOTOWNED;
+        per[s->gindex - pe->firstShard].push_back(pos[i]);
+    }
+    int busy = 0;
+    for (auto& v : per) busy += !v.empty();
+    if (busy <= 1) {
+        for (size_t k = 0; k < per.size(); ++k)
+            if (!per[k].empty()) return compute_shard(pe, pe->shards[k].get(), per[k].data(),
+                                                      (int32_t)per[k].size());
+        return SHD_PE_OK;
+    }
+    std::vector<int> rcs(per.size(), SHD_PE_OK);
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < per.size(); ++k) {
+        if (per[k].empty()) continue;
+        th.emplace_back([&, k] {
+            rcs[k] = compute_shard(pe, pe->shards[k].get(), per[k].data(), (int32_t)per[k].size());
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int r : rcs)
+        if (r) return r;
+    return SHD_PE_OK;
+}
+
+static bool row_done(const ShdPe* pe, int32_t p) {
+    return pe->rowDone[p].load(std::memory_order_acquire) != 0;
 }
 
 extern "C" int shd_pe_compute_positions(ShdPe* pe, int32_t start, int32_t count) {
     if (!pe || start < 0 || count < 0 || (int64_t)start + count > (int64_t)pe->attached.size())
         return SHD_PE_EINVAL;
+    if (count && (start < pe->ownStart || start + count > pe->ownEnd)) return SHD_PE_ENOTOWNED;
     std::vector<int32_t> pos(count);
     for (int32_t i = 0; i < count; ++i) pos[i] = start + i;
     std::lock_guard<std::mutex> lk(pe->mu);
@@ -681,7 +873,7 @@ extern "C" int shd_pe_compute_positions(ShdPe* pe, int32_t start, int32_t count)
 
 extern "C" int shd_pe_compute_all(ShdPe* pe) {
     if (!pe) return SHD_PE_EINVAL;
-    return shd_pe_compute_positions(pe, 0, (int32_t)pe->attached.size());
+    return shd_pe_compute_positions(pe, pe->ownStart, pe->ownEnd - pe->ownStart);
 }
 
 extern "C" int shd_pe_compute_rows(ShdPe* pe, const int32_t* src, int32_t count) {
@@ -690,9 +882,51 @@ extern "C" int shd_pe_compute_rows(ShdPe* pe, const int32_t* src, int32_t count)
     for (int32_t i = 0; i < count; ++i) {
         if (src[i] < 0 || src[i] >= pe->hg.n || pe->posOf[src[i]] < 0) return SHD_PE_ENOTATTACHED;
         pos[i] = pe->posOf[src[i]];
+        if (pos[i] < pe->ownStart || pos[i] >= pe->ownEnd) return SHD_PE_ENOTOWNED;
     }
     std::lock_guard<std::mutex> lk(pe->mu);
     return compute_positions_locked(pe, pos.data(), count);
+}
+
+// Compute whatever rows of [start, start+count) are owned here and missing.
+static int ensure_rows(ShdPe* pe, int32_t start, int32_t count) {
+    bool all = true;
+    for (int32_t i = start; i < start + count && all; ++i) all = row_done(pe, i);
+    if (all) return SHD_PE_OK;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    std::vector<int32_t> todo;
+    for (int32_t i = start; i < start + count; ++i) {
+        if (row_done(pe, i)) continue;
+        if (i < pe->ownStart || i >= pe->ownEnd) return SHD_PE_ENOTOWNED;
+        todo.push_back(i);
+    }
+    return compute_positions_locked(pe, todo.data(), (int32_t)todo.size());
+}
+
+// A contiguous run of table rows readable from one device table.
+struct Piece {
+    const DevTable* tab;
+    hipStream_t stream;
+    int device;
+    int32_t start, count;   // table positions
+};
+
+static int table_pieces(ShdPe* pe, int32_t start, int32_t count, std::vector<Piece>& out) {
+    out.clear();
+    if (pe->gathered) {
+        Shard* s = pe->shards[0].get();
+        out.push_back(Piece{&s->full, s->copyStream, s->device, start, count});
+        return SHD_PE_OK;
+    }
+    int32_t p = start;
+    while (p < start + count) {
+        Shard* s = owner_of(pe, p);
+        if (!s || !s->tableReady) return SHD_PE_ENOTOWNED;
+        const int32_t end = std::min(start + count, s->rowStart + s->rowCount);
+        out.push_back(Piece{&s->tab, s->copyStream, s->device, p, end - p});
+        p = end;
+    }
+    return SHD_PE_OK;
 }
 
 static int get_rows_staged(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
@@ -704,81 +938,81 @@ extern "C" int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double*
     const int32_t p = pe->posOf[srcVertex];
     if (p < 0) return SHD_PE_ENOTATTACHED;
     if (pred && !pe->opt.storePred) return SHD_PE_EINVAL;
-    if (!pe->rowDone[p]) {
-        std::lock_guard<std::mutex> lk(pe->mu);
-        if (!pe->rowDone[p]) {
-            int rc = compute_positions_locked(pe, &p, 1);
-            if (rc) return rc;
-        }
-    }
+    int rc = ensure_rows(pe, p, 1);
+    if (rc) return rc;
     return get_rows_staged(pe, p, 1, lat, rel, hops, pred, flags);
 }
 
 // Rows [start, start+count) -> caller host buffers through two pinned
-// staging buffers: block b's five field copies run on copyStream while the
-// host copies block b-1 out of the other buffer.
+// staging buffers: block b's five field copies run on the copy stream while
+// the host copies block b-1 out of the other buffer.
 static int get_rows_staged(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
                            int32_t* hops, int32_t* pred, uint8_t* flags) {
     const size_t T = pe->attached.size();
     const size_t perRow = T * (8 + 8 + 4 + 4 + 1);
     std::lock_guard<std::mutex> lk(pe->copyMu);
-    HIPCHK(hipSetDevice(pe->device));
-    if (!pe->copyStream) HIPCHK(hipStreamCreateWithFlags(&pe->copyStream, hipStreamNonBlocking));
+    std::vector<Piece> pieces;
+    int rc = table_pieces(pe, start, count, pieces);
+    if (rc) return rc;
     if (!pe->stage[0]) {
         const size_t want = std::max<size_t>(perRow, (size_t)32 << 20);
-        for (auto& h : pe->stage) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h), want));
+        for (auto& h : pe->stage)
+            HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h), want, hipHostMallocPortable));
         pe->stageBytes = want;
     }
     const int32_t B = (int32_t)std::max<size_t>(1, pe->stageBytes / perRow);
-    struct Blk { int32_t r0, n; };
-    auto issue = [&](int buf, Blk b) -> int {
-        unsigned char* h = pe->stage[buf];
-        const size_t off = ((size_t)start + b.r0) * T, cells = (size_t)b.n * T;
-        unsigned char* q = h;
-        if (lat) { HIPCHK(hipMemcpyAsync(q, pe->tab.lat + off, cells * 8, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 8; }
-        if (rel) { HIPCHK(hipMemcpyAsync(q, pe->tab.rel + off, cells * 8, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 8; }
-        if (hops) { HIPCHK(hipMemcpyAsync(q, pe->tab.hops + off, cells * 4, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 4; }
-        if (pred) { HIPCHK(hipMemcpyAsync(q, pe->tab.pred + off, cells * 4, hipMemcpyDeviceToHost, pe->copyStream)); q += cells * 4; }
-        if (flags) { HIPCHK(hipMemcpyAsync(q, pe->tab.flags + off, cells, hipMemcpyDeviceToHost, pe->copyStream)); }
-        return SHD_PE_OK;
-    };
-    auto drain = [&](int buf, Blk b) {
-        const unsigned char* q = pe->stage[buf];
-        const size_t o = (size_t)b.r0 * T, cells = (size_t)b.n * T;
-        if (lat) { std::memcpy(lat + o, q, cells * 8); q += cells * 8; }
-        if (rel) { std::memcpy(rel + o, q, cells * 8); q += cells * 8; }
-        if (hops) { std::memcpy(hops + o, q, cells * 4); q += cells * 4; }
-        if (pred) { std::memcpy(pred + o, q, cells * 4); q += cells * 4; }
-        if (flags) std::memcpy(flags + o, q, cells);
-    };
-    hipEvent_t done[2];
-    HIPCHK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
-    if (hipEventCreateWithFlags(&done[1], hipEventDisableTiming) != hipSuccess) {
-        (void)hipEventDestroy(done[0]);
-        return SHD_PE_EHIP;
-    }
-    int rc = SHD_PE_OK;
-    Blk prev{0, 0};
-    int buf = 0;
-    for (int32_t r0 = 0; r0 < count && rc == SHD_PE_OK; r0 += B) {
-        const Blk cur{r0, std::min(B, count - r0)};
-        if ((rc = issue(buf, cur)) == SHD_PE_OK &&
-            hipEventRecord(done[buf], pe->copyStream) != hipSuccess)
-            rc = SHD_PE_EHIP;
+    for (const Piece& pc : pieces) {
+        HIPCHK(hipSetDevice(pc.device));
+        const DevTable& tb = *pc.tab;
+        struct Blk { int32_t r0, n; };   // r0 relative to pc.start
+        auto issue = [&](int buf, Blk b) -> int {
+            unsigned char* q = pe->stage[buf];
+            const size_t off = ((size_t)(pc.start - tb.rowStart) + b.r0) * T, cells = (size_t)b.n * T;
+            if (lat) { HIPCHK(hipMemcpyAsync(q, tb.lat + off, cells * 8, hipMemcpyDeviceToHost, pc.stream)); q += cells * 8; }
+            if (rel) { HIPCHK(hipMemcpyAsync(q, tb.rel + off, cells * 8, hipMemcpyDeviceToHost, pc.stream)); q += cells * 8; }
+            if (hops) { HIPCHK(hipMemcpyAsync(q, tb.hops + off, cells * 4, hipMemcpyDeviceToHost, pc.stream)); q += cells * 4; }
+            if (pred) { HIPCHK(hipMemcpyAsync(q, tb.pred + off, cells * 4, hipMemcpyDeviceToHost, pc.stream)); q += cells * 4; }
+            if (flags) { HIPCHK(hipMemcpyAsync(q, tb.flags + off, cells, hipMemcpyDeviceToHost, pc.stream)); }
+            return SHD_PE_OK;
+        };
+        auto drain = [&](int buf, Blk b) {
+            const unsigned char* q = pe->stage[buf];
+            const size_t o = ((size_t)(pc.start - start) + b.r0) * T, cells = (size_t)b.n * T;
+            if (lat) { std::memcpy(lat + o, q, cells * 8); q += cells * 8; }
+            if (rel) { std::memcpy(rel + o, q, cells * 8); q += cells * 8; }
+            if (hops) { std::memcpy(hops + o, q, cells * 4); q += cells * 4; }
+            if (pred) { std::memcpy(pred + o, q, cells * 4); q += cells * 4; }
+            if (flags) std::memcpy(flags + o, q, cells);
+        };
+        hipEvent_t done[2];
+        HIPCHK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+        if (hipEventCreateWithFlags(&done[1], hipEventDisableTiming) != hipSuccess) {
+            (void)hipEventDestroy(done[0]);
+            return SHD_PE_EHIP;
+        }
+        Blk prev{0, 0};
+        int buf = 0;
+        for (int32_t r0 = 0; r0 < pc.count && rc == SHD_PE_OK; r0 += B) {
+            const Blk cur{r0, std::min(B, pc.count - r0)};
+            if ((rc = issue(buf, cur)) == SHD_PE_OK &&
+                hipEventRecord(done[buf], pc.stream) != hipSuccess)
+                rc = SHD_PE_EHIP;
+            if (rc == SHD_PE_OK && prev.n) {
+                if (hipEventSynchronize(done[buf ^ 1]) != hipSuccess) rc = SHD_PE_EHIP;
+                else drain(buf ^ 1, prev);
+            }
+            prev = cur;
+            buf ^= 1;
+        }
         if (rc == SHD_PE_OK && prev.n) {
             if (hipEventSynchronize(done[buf ^ 1]) != hipSuccess) rc = SHD_PE_EHIP;
             else drain(buf ^ 1, prev);
         }
-        prev = cur;
-        buf ^= 1;
+        (void)hipStreamSynchronize(pc.stream);
+        (void)hipEventDestroy(done[0]);
+        (void)hipEventDestroy(done[1]);
+        if (rc) return rc;
     }
-    if (rc == SHD_PE_OK && prev.n) {
-        if (hipEventSynchronize(done[buf ^ 1]) != hipSuccess) rc = SHD_PE_EHIP;
-        else drain(buf ^ 1, prev);
-    }
-    (void)hipStreamSynchronize(pe->copyStream);
-    (void)hipEventDestroy(done[0]);
-    (void)hipEventDestroy(done[1]);
     return rc;
 }
 
@@ -788,18 +1022,8 @@ extern "C" int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* 
         return SHD_PE_EINVAL;
     if (pred && !pe->opt.storePred) return SHD_PE_EINVAL;
     if (count == 0) return SHD_PE_OK;
-    bool all = true;
-    for (int32_t i = start; i < start + count; ++i) all = all && pe->rowDone[i];
-    if (!all) {
-        std::lock_guard<std::mutex> lk(pe->mu);
-        std::vector<int32_t> todo;
-        for (int32_t i = start; i < start + count; ++i)
-            if (!pe->rowDone[i]) todo.push_back(i);
-        if (!todo.empty()) {
-            int rc = compute_positions_locked(pe, todo.data(), (int32_t)todo.size());
-            if (rc) return rc;
-        }
-    }
+    int rc = ensure_rows(pe, start, count);
+    if (rc) return rc;
     return get_rows_staged(pe, start, count, lat, rel, hops, pred, flags);
 }
 
@@ -807,14 +1031,211 @@ extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, 
                                        double* dRel, int32_t* dHops, uint8_t* dFlags) {
     if (!pe || start < 0 || count < 0 || (int64_t)start + count > (int64_t)pe->attached.size())
         return SHD_PE_EINVAL;
-    if (!pe->tableReady) return SHD_PE_EINVAL;
-    const size_t T = pe->attached.size(), off = (size_t)start * T, cells = (size_t)count * T;
-    HIPCHK(hipSetDevice(pe->device));
-    if (dLat) HIPCHK(hipMemcpyAsync(dLat, pe->tab.lat + off, cells * 8, hipMemcpyDeviceToDevice, pe->stream));
-    if (dRel) HIPCHK(hipMemcpyAsync(dRel, pe->tab.rel + off, cells * 8, hipMemcpyDeviceToDevice, pe->stream));
-    if (dHops) HIPCHK(hipMemcpyAsync(dHops, pe->tab.hops + off, cells * 4, hipMemcpyDeviceToDevice, pe->stream));
-    if (dFlags) HIPCHK(hipMemcpyAsync(dFlags, pe->tab.flags + off, cells, hipMemcpyDeviceToDevice, pe->stream));
-    HIPCHK(hipStreamSynchronize(pe->stream));
+    if (count == 0) return SHD_PE_OK;
+    int rc = ensure_rows(pe, start, count);       // same contract as shd_pe_get_rows
+    if (rc) return rc;
+    std::vector<Piece> pieces;
+    if ((rc = table_pieces(pe, start, count, pieces))) return rc;
+    const size_t T = pe->attached.size();
+    for (const Piece& pc : pieces) {
+        HIPCHK(hipSetDevice(pc.device));
+        const DevTable& tb = *pc.tab;
+        const size_t off = (size_t)(pc.start - tb.rowStart) * T, cells = (size_t)pc.count * T;
+        const size_t o = (size_t)(pc.start - start) * T;
+        if (dLat) HIPCHK(hipMemcpyAsync(dLat + o, tb.lat + off, cells * 8, hipMemcpyDeviceToDevice, pc.stream));
+        if (dRel) HIPCHK(hipMemcpyAsync(dRel + o, tb.rel + off, cells * 8, hipMemcpyDeviceToDevice, pc.stream));
+        if (dHops) HIPCHK(hipMemcpyAsync(dHops + o, tb.hops + off, cells * 4, hipMemcpyDeviceToDevice, pc.stream));
+        if (dFlags) HIPCHK(hipMemcpyAsync(dFlags + o, tb.flags + off, cells, hipMemcpyDeviceToDevice, pc.stream));
+        HIPCHK(hipStreamSynchronize(pc.stream));
+    }
+    return SHD_PE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Gather: the whole table on every device of this engine (and, with a
+// cross-process communicator, of every engine).
+// ---------------------------------------------------------------------------
+static int ensure_full(ShdPe* pe, Shard* s, Shard* owner) {
+    if (s != owner) { s->full = owner->full; return SHD_PE_OK; }
+    if (s->full.lat) return SHD_PE_OK;
+    const size_t T = pe->attached.size(), cells = T * T;
+    if (pe->G == 1) { s->full = s->tab; return SHD_PE_OK; }   // the shard is the table
+    HIPCHK(hipSetDevice(s->device));
+    int rc;
+    void *lat, *rel, *hops, *flags, *pred = nullptr;
+    if ((rc = dev_alloc(s, &lat, cells * 8)) || (rc = dev_alloc(s, &rel, cells * 8)) ||
+        (rc = dev_alloc(s, &hops, cells * 4)) || (rc = dev_alloc(s, &flags, cells)))
+        return rc;
+    if (pe->opt.storePred && (rc = dev_alloc(s, &pred, cells * 4))) return rc;
+    s->full = DevTable{(double*)lat, (double*)rel, (int32_t*)hops, (int32_t*)pred, (uint8_t*)flags,
+                       (int64_t)T, 0};
+    return SHD_PE_OK;
+}
+
+struct Field { size_t off; size_t esize; ncclDataType_t type; };
+
+static void table_fields(const ShdPe* pe, std::vector<Field>& f) {
+    f = {{offsetof(DevTable, lat), 8, ncclUint64}, {offsetof(DevTable, rel), 8, ncclUint64},
+         {offsetof(DevTable, hops), 4, ncclInt32}, {offsetof(DevTable, flags), 1, ncclUint8}};
+    if (pe->opt.storePred) f.push_back({offsetof(DevTable, pred), 4, ncclInt32});
+}
+
+static void* field_ptr(const DevTable& t, const Field& f) {
+    return *reinterpret_cast<void* const*>(reinterpret_cast<const char*>(&t) + f.off);
+}
+
+static int gather_locked(ShdPe* pe) {
+    const int32_t T = (int32_t)pe->attached.size();
+    std::vector<int32_t> all;
+    for (int32_t p = pe->ownStart; p < pe->ownEnd; ++p)
+        if (!row_done(pe, p)) all.push_back(p);
+    int rc = compute_positions_locked(pe, all.data(), (int32_t)all.size());
+    if (rc) return rc;
+    for (auto& s : pe->shards) if ((rc = ensure_table(pe, s.get()))) return rc;
+    // one full table per distinct device, owned by its first shard
+    for (auto& s : pe->shards) {
+        Shard* owner = nullptr;
+        for (auto& o : pe->shards)
+            if (o->device == s->device) { owner = o.get(); break; }
+        if ((rc = ensure_full(pe, s.get(), owner))) return rc;
+    }
+    std::vector<Field> fields;
+    table_fields(pe, fields);
+    const size_t ts = (size_t)T;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    Shard* s0 = pe->shards[0].get();
+    HIPCHK(hipSetDevice(s0->device));
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s0->stream));
+    if (pe->G == 1) {
+        // nothing to exchange
+    } else if (pe->xcomm) {
+        // cross-process: every process owns one shard (nDevices == 1); the
+        // group of per-shard broadcasts is an all-gather with shard-sized
+        // blocks landing in place (rows are contiguous per shard)
+        Shard* s = s0;
+        if (ncclGroupStart() != ncclSuccess) return SHD_PE_ECOMM;
+        for (int g = 0; g < pe->G && rc == SHD_PE_OK; ++g) {
+            const size_t r0 = (size_t)pe->bounds[g], nr = (size_t)(pe->bounds[g + 1] - pe->bounds[g]);
+            if (!nr) continue;
+            for (const Field& f : fields) {
+                char* dst = (char*)field_ptr(s->full, f) + r0 * ts * f.esize;
+                const void* src = g == s->gindex ? field_ptr(s->tab, f) : (const void*)dst;
+                if (ncclBroadcast(src, dst, nr * ts, f.type, g, pe->xcomm, s->stream) != ncclSuccess)
+                    rc = SHD_PE_ECOMM;
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) rc = SHD_PE_ECOMM;
+        if (rc) return rc;
+    } else {
+        bool distinct = true;
+        for (size_t i = 0; i < pe->shards.size(); ++i)
+            for (size_t j = 0; j < i; ++j)
+                if (pe->shards[i]->device == pe->shards[j]->device) distinct = false;
+        if (distinct) {
+            // in-process RCCL over xGMI: one communicator per device
+            if (!s0->comm) {
+                std::vector<ncclComm_t> comms(pe->shards.size());
+                std::vector<int> devs;
+                for (auto& s : pe->shards) devs.push_back(s->device);
+                if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess)
+                    return SHD_PE_ECOMM;
+                for (size_t i = 0; i < comms.size(); ++i) pe->shards[i]->comm = comms[i];
+            }
+            if (ncclGroupStart() != ncclSuccess) return SHD_PE_ECOMM;
+            for (size_t r = 0; r < pe->shards.size(); ++r) {
+                Shard* root = pe->shards[r].get();
+                const size_t r0 = (size_t)root->rowStart, nr = (size_t)root->rowCount;
+                if (!nr) continue;
+                for (auto& sp : pe->shards) {
+                    Shard* s = sp.get();
+                    for (const Field& f : fields) {
+                        char* dst = (char*)field_ptr(s->full, f) + r0 * ts * f.esize;
+                        const void* src = s == root ? field_ptr(root->tab, f) : (const void*)dst;
+                        if (ncclBroadcast(src, dst, nr * ts, f.type, (int)r, s->comm, s->stream) !=
+                            ncclSuccess)
+                            rc = SHD_PE_ECOMM;
+                    }
+                }
+            }
+            if (ncclGroupEnd() != ncclSuccess) rc = SHD_PE_ECOMM;
+            if (rc) return rc;
+        } else {
+            // logical shards sharing a device (tests): device / peer copies
+            for (auto& src : pe->shards) {
+                if (!src->rowCount) continue;
+                for (auto& dstS : pe->shards) {
+                    if (!dstS->fullOwner) continue;
+                    HIPCHK(hipSetDevice(dstS->device));
+                    for (const Field& f : fields) {
+                        char* dst = (char*)field_ptr(dstS->full, f) + (size_t)src->rowStart * ts * f.esize;
+                        HIPCHK(hipMemcpyAsync(dst, field_ptr(src->tab, f),
+                                              (size_t)src->rowCount * ts * f.esize,
+                                              hipMemcpyDeviceToDevice, dstS->stream));
+                    }
+                }
+            }
+        }
+    }
+    for (auto& s : pe->shards) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
+    HIPCHK(hipSetDevice(s0->device));
+    HIPCHK(hipEventRecord(e1, s0->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    pe->msGather += elapsed(e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (int32_t p = 0; p < T; ++p) pe->rowDone[p].store(1, std::memory_order_release);
+    pe->gathered = true;
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_gather(ShdPe* pe) {
+    if (!pe) return SHD_PE_EINVAL;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    std::lock_guard<std::mutex> lk2(pe->copyMu);
+    if (pe->G > 1 && pe->opt.shardCount > 1 && !pe->xcomm) return SHD_PE_ECOMM;
+    return gather_locked(pe);
+}
+
+extern "C" int shd_pe_comm_unique_id(void* out, int32_t bytes) {
+    if (!out || bytes < (int32_t)sizeof(ncclUniqueId)) return SHD_PE_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SHD_PE_ECOMM;
+    std::memcpy(out, &id, sizeof(id));
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_comm_init(ShdPe* pe, const void* uniqueId, int32_t bytes) {
+    if (!pe || !uniqueId || bytes < (int32_t)sizeof(ncclUniqueId)) return SHD_PE_EINVAL;
+    if (pe->opt.nDevices != 1 || pe->opt.shardCount < 2) return SHD_PE_EINVAL;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    if (pe->xcomm) return SHD_PE_OK;
+    ncclUniqueId id;
+    std::memcpy(&id, uniqueId, sizeof(id));
+    if (hipSetDevice(pe->shards[0]->device) != hipSuccess) return SHD_PE_EHIP;
+    if (ncclCommInitRank(&pe->xcomm, pe->opt.shardCount, id, pe->opt.shardIndex) != ncclSuccess) {
+        pe->xcomm = nullptr;
+        return SHD_PE_ECOMM;
+    }
+    return SHD_PE_OK;
+}
+
+extern "C" int32_t shd_pe_num_shards(const ShdPe* pe) { return pe ? pe->G : 0; }
+
+extern "C" int shd_pe_shard_bounds(const ShdPe* pe, int32_t* bounds) {
+    if (!pe || !bounds) return SHD_PE_EINVAL;
+    std::memcpy(bounds, pe->bounds.data(), pe->bounds.size() * sizeof(int32_t));
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_owned_range(const ShdPe* pe, int32_t* start, int32_t* count) {
+    if (!pe) return SHD_PE_EINVAL;
+    if (start) *start = pe->ownStart;
+    if (count) *count = pe->ownEnd - pe->ownStart;
     return SHD_PE_OK;
 }
 
@@ -841,28 +1262,29 @@ __global__ __launch_bounds__(256) void k_stream_copy(const v4u* __restrict__ a,
 
 extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbps) {
     if (!pe || !gbps || bytes < (1 << 20) || iters < 1) return SHD_PE_EINVAL;
-    HIPCHK(hipSetDevice(pe->device));
+    Shard* sh = pe->shards[0].get();
+    HIPCHK(hipSetDevice(sh->device));
     const size_t n = (size_t)bytes / 16;
     void *a = nullptr, *b = nullptr;
     if (hipMalloc(&a, n * 16) != hipSuccess) return SHD_PE_ENOMEM;
     if (hipMalloc(&b, n * 16) != hipSuccess) { (void)hipFree(a); return SHD_PE_ENOMEM; }
     int rc = SHD_PE_OK;
-    const int grid = pe->numCUs * env_int("SHDPE_STREAM_WG_PER_CU", 4);
-    if (hipMemsetAsync(a, 0, n * 16, pe->stream) != hipSuccess) rc = SHD_PE_EHIP;
+    const int grid = sh->numCUs * pe->tu.streamWgPerCU;
+    if (hipMemsetAsync(a, 0, n * 16, sh->stream) != hipSuccess) rc = SHD_PE_EHIP;
     if (!rc) {
-        hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, pe->stream, (const v4u*)a,
+        hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, sh->stream, (const v4u*)a,
                            (v4u*)b, n);   // warm-up
-        (void)hipEventRecord(pe->evA, pe->stream);
+        (void)hipEventRecord(sh->evA, sh->stream);
         for (int i = 0; i < iters; ++i)
-            hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, pe->stream,
+            hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, sh->stream,
                                (const v4u*)a, (v4u*)b, n);
-        (void)hipEventRecord(pe->evB, pe->stream);
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(pe->stream) != hipSuccess)
+        (void)hipEventRecord(sh->evB, sh->stream);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(sh->stream) != hipSuccess)
             rc = SHD_PE_EHIP;
     }
     if (!rc) {
         float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, pe->evA, pe->evB);
+        (void)hipEventElapsedTime(&ms, sh->evA, sh->evB);
         *gbps = ms > 0.f ? 2.0 * (double)n * 16.0 * iters / (ms * 1e-3) / 1e9 : 0.0;
     }
     (void)hipFree(a);
@@ -872,22 +1294,17 @@ extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, 
 
 extern "C" int shd_pe_synchronize(ShdPe* pe) {
     if (!pe) return SHD_PE_EINVAL;
-    HIPCHK(hipSetDevice(pe->device));
-    HIPCHK(hipStreamSynchronize(pe->stream));
+    for (auto& s : pe->shards) {
+        HIPCHK(hipSetDevice(s->device));
+        HIPCHK(hipStreamSynchronize(s->stream));
+    }
     return SHD_PE_OK;
 }
 
 extern "C" void shd_pe_destroy(ShdPe* pe) {
     if (!pe) return;
-    if (!pe->allocs.empty() || pe->stream) (void)hipSetDevice(pe->device);
-    if (pe->stream) (void)hipStreamSynchronize(pe->stream);
-    for (void* p : pe->allocs) (void)hipFree(p);
-    if (pe->ev0) (void)hipEventDestroy(pe->ev0);
-    if (pe->ev1) (void)hipEventDestroy(pe->ev1);
-    if (pe->evA) (void)hipEventDestroy(pe->evA);
-    if (pe->evB) (void)hipEventDestroy(pe->evB);
-    if (pe->stream) (void)hipStreamDestroy(pe->stream);
-    if (pe->copyStream) (void)hipStreamDestroy(pe->copyStream);
+    for (auto& s : pe->shards) destroy_shard(s.get());
+    if (pe->xcomm) (void)ncclCommDestroy(pe->xcomm);
     for (unsigned char* h : pe->stage)
         if (h) (void)hipHostFree(h);
     delete pe;
@@ -907,22 +1324,46 @@ extern "C" int shd_pe_attached(const ShdPe* pe, int32_t* out) {
 
 extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
     if (!pe || !out) return SHD_PE_EINVAL;
-    *out = pe->stats;
+    ShdPeStats t = pe->shards[0]->stats;
+    for (size_t i = 1; i < pe->shards.size(); ++i) {
+        const ShdPeStats& s = pe->shards[i]->stats;
+        t.rowsComputed += s.rowsComputed;
+        t.rowsExact += s.rowsExact;
+        t.arcsRelaxed += s.arcsRelaxed;
+        t.msSparseKernel += s.msSparseKernel;
+        t.msExactKernel += s.msExactKernel;
+        t.msDirectKernel += s.msDirectKernel;
+        t.msTotal = std::max(t.msTotal, s.msTotal);   // shards run concurrently
+        t.launchesSparse += s.launchesSparse;
+        t.launchesExact += s.launchesExact;
+        t.launchesDirect += s.launchesDirect;
+        t.msDenseKernel += s.msDenseKernel;
+        t.launchesDense += s.launchesDense;
+        t.denseSweeps += s.denseSweeps;
+        t.denseFlops += s.denseFlops;
+    }
+    t.nShards = (int32_t)pe->shards.size();
+    t.msGather = pe->msGather;
+    *out = t;
     return SHD_PE_OK;
 }
 
 extern "C" int shd_pe_reset_stats(ShdPe* pe) {
     if (!pe) return SHD_PE_EINVAL;
-    ShdPeStats keep = pe->stats;
-    std::memset(&pe->stats, 0, sizeof(pe->stats));
-    pe->stats.mode = keep.mode;
-    pe->stats.isComplete = keep.isComplete;
-    pe->stats.nVertices = keep.nVertices;
-    pe->stats.nArcs = keep.nArcs;
-    pe->stats.nAttached = keep.nAttached;
-    pe->stats.deltaUsed = keep.deltaUsed;
-    pe->stats.batched = keep.batched;
-    pe->stats.batchLanes = keep.batchLanes;
+    for (auto& sp : pe->shards) {
+        ShdPeStats& st = sp->stats;
+        ShdPeStats keep = st;
+        std::memset(&st, 0, sizeof(st));
+        st.mode = keep.mode;
+        st.isComplete = keep.isComplete;
+        st.nVertices = keep.nVertices;
+        st.nArcs = keep.nArcs;
+        st.nAttached = keep.nAttached;
+        st.deltaUsed = keep.deltaUsed;
+        st.batched = keep.batched;
+        st.batchLanes = keep.batchLanes;
+    }
+    pe->msGather = 0.0;
     return SHD_PE_OK;
 }
 

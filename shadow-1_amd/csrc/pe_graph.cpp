@@ -10,8 +10,12 @@
 #include "pe_graph.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
+#include <cstdint>
+#include <thread>
 #include <utility>
+#include <vector>
 
 namespace shdpe {
 
@@ -25,33 +29,62 @@ int64_t HostGraph::findArc(int32_t from, int32_t to) const {
     return -1;
 }
 
-static int sort_rows(int32_t n, std::vector<int32_t>& ptr, std::vector<int32_t>& colv,
-                     std::vector<double>& latv, std::vector<double>& relv) {
-    std::vector<std::pair<int32_t, int32_t>> tmp;
-    std::vector<double> l2, r2;
-    for (int32_t v = 0; v < n; ++v) {
-        const int32_t b = ptr[v], e = ptr[v + 1];
-        bool sorted = true;
-        for (int32_t a = b + 1; a < e; ++a)
-            if (colv[a - 1] >= colv[a]) { sorted = false; break; }
-        if (sorted) continue;
-        tmp.clear();
-        for (int32_t a = b; a < e; ++a) tmp.emplace_back(colv[a], a);
-        std::sort(tmp.begin(), tmp.end());
-        for (size_t k = 1; k < tmp.size(); ++k)
-            if (tmp[k].first == tmp[k - 1].first) return SHD_PE_EMULTI;
-        l2.resize(tmp.size());
-        r2.resize(tmp.size());
-        for (size_t k = 0; k < tmp.size(); ++k) {
-            l2[k] = latv[tmp[k].second];
-            r2[k] = relv[tmp[k].second];
+// ---- deterministic parallel passes (results independent of thread count) --
+static int host_threads() {
+    const unsigned h = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, h ? h : 1u));
+}
+
+// f(chunk, lo, hi) over nChunks fixed chunks of [0, n), chunks dealt to
+// threads; `work` (total element visits) below 2^20 runs inline
+template <class F>
+static void par_chunks(int64_t n, int nChunks, int64_t work, F f) {
+    const int nt = std::min(host_threads(), nChunks);
+    auto run = [&](int t) {
+        for (int c = t; c < nChunks; c += nt) f(c, n * c / nChunks, n * (c + 1) / nChunks);
+    };
+    if (nt <= 1 || work < (1 << 20)) { run(0); if (nt > 1) for (int t = 1; t < nt; ++t) run(t); return; }
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(run, t);
+    run(0);
+    for (auto& x : th) x.join();
+}
+
+// Sort each row by neighbour id (igraph incidence order); a repeated
+// neighbour is a parallel edge -> SHD_PE_EMULTI.
+static int sort_rows(int32_t n, const std::vector<int32_t>& ptr, hvec<int32_t>& colv,
+                     hvec<double>& latv, hvec<double>& relv) {
+    const int nc = 64;
+    std::vector<int> rcs(nc, SHD_PE_OK);
+    par_chunks(n, nc, (int64_t)colv.size(), [&](int c, int64_t v0, int64_t v1) {
+        std::vector<std::pair<int32_t, int32_t>> tmp;
+        std::vector<double> l2, r2;
+        for (int64_t v = v0; v < v1; ++v) {
+            const int32_t b = ptr[v], e = ptr[v + 1];
+            bool sorted = true;
+            for (int32_t a = b + 1; a < e; ++a)
+                if (colv[a - 1] >= colv[a]) { sorted = false; break; }
+            if (sorted) continue;
+            tmp.clear();
+            for (int32_t a = b; a < e; ++a) tmp.emplace_back(colv[a], a);
+            std::sort(tmp.begin(), tmp.end());
+            for (size_t k = 1; k < tmp.size(); ++k)
+                if (tmp[k].first == tmp[k - 1].first) { rcs[c] = SHD_PE_EMULTI; return; }
+            l2.resize(tmp.size());
+            r2.resize(tmp.size());
+            for (size_t k = 0; k < tmp.size(); ++k) {
+                l2[k] = latv[tmp[k].second];
+                r2[k] = relv[tmp[k].second];
+            }
+            for (size_t k = 0; k < tmp.size(); ++k) {
+                colv[b + k] = tmp[k].first;
+                latv[b + k] = l2[k];
+                relv[b + k] = r2[k];
+            }
         }
-        for (size_t k = 0; k < tmp.size(); ++k) {
-            colv[b + k] = tmp[k].first;
-            latv[b + k] = l2[k];
-            relv[b + k] = r2[k];
-        }
-    }
+    });
+    for (int r : rcs)
+        if (r) return r;
     return SHD_PE_OK;
 }
 
@@ -77,36 +110,66 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
             g->vrel[v] = 1.0 - p;                 // (1.0f - packetLoss), :1444
         }
     }
-    int64_t nonLoop = 0;
-    std::vector<int64_t> deg(n + 1, 0);
-    for (int64_t e = 0; e < m; ++e) {
-        const int32_t a = d->edgeFrom[e], b = d->edgeTo[e];
-        if (a < 0 || a >= n || b < 0 || b >= n) return SHD_PE_EINVAL;
-        const double L = d->edgeLatency[e], p = d->edgePacketLoss[e];
-        if (!(L > 0.0)) return SHD_PE_EINVAL;                  // :1070 (NaN fails too)
-        if (!(p >= 0.0 && p <= 1.0)) return SHD_PE_EINVAL;     // :1090
-        if (a == b) {
+    // Pass 1 (chunks of the edge list): first invalid edge, self-loops in
+    // edge order, and per-chunk arc counts per row.  The serial semantics --
+    // the first bad edge in edge order decides the error -- are kept by
+    // taking the minimum over chunks.
+    const int NC = (int)std::max<int64_t>(1, std::min<int64_t>(64, m / 4096 + 1));
+    std::vector<int64_t> firstBad(NC, INT64_MAX);
+    std::vector<std::vector<int64_t>> loops(NC);
+    std::vector<std::vector<int32_t>> cnt(NC);
+    par_chunks(m, NC, m, [&](int c, int64_t e0, int64_t e1) {
+        std::vector<int32_t>& k = cnt[c];
+        k.assign(n, 0);
+        for (int64_t e = e0; e < e1; ++e) {
+            const int32_t a = d->edgeFrom[e], b = d->edgeTo[e];
+            const double L = d->edgeLatency[e], p = d->edgePacketLoss[e];
+            if (a < 0 || a >= n || b < 0 || b >= n || !(L > 0.0) ||   // :1070 (NaN fails too)
+                !(p >= 0.0 && p <= 1.0)) {                            // :1090
+                firstBad[c] = e;
+                return;
+            }
+            if (a == b) { loops[c].push_back(e); continue; }
+            k[a]++;
+            if (!g->directed) k[b]++;
+        }
+    });
+    int64_t bad = INT64_MAX;
+    for (int64_t x : firstBad) bad = std::min(bad, x);
+    for (int c = 0; c < NC; ++c) {
+        for (int64_t e : loops[c]) {
+            if (e > bad) break;
+            const int32_t a = d->edgeFrom[e];
             if (g->hasSelf[a]) return SHD_PE_EMULTI;
             g->hasSelf[a] = 1;
-            g->selfLat[a] = L;
-            g->selfRel[a] = 1.0 - p;                            // :437
-            continue;
+            g->selfLat[a] = d->edgeLatency[e];
+            g->selfRel[a] = 1.0 - d->edgePacketLoss[e];                 // :437
         }
-        ++nonLoop;
-        deg[a + 1]++;
-        if (!g->directed) deg[b + 1]++;
     }
-    const int64_t nArcs = g->directed ? nonLoop : 2 * nonLoop;
-    if (nArcs >= (int64_t)INT32_MAX) return SHD_PE_EINVAL;
-    for (int32_t v = 0; v < n; ++v) deg[v + 1] += deg[v];
+    if (bad != INT64_MAX) return SHD_PE_EINVAL;
+    // row pointers; chunk c writes row v from offset rowPtr[v] + (arcs of v
+    // in chunks < c): every row keeps edge-id order, as the serial fill
     g->rowPtr.assign(n + 1, 0);
-    for (int32_t v = 0; v <= n; ++v) g->rowPtr[v] = (int32_t)deg[v];
-    g->col.assign(nArcs, 0);
-    g->lat.assign(nArcs, 0.0);
-    g->rel.assign(nArcs, 0.0);
     {
-        std::vector<int32_t> fill(g->rowPtr.begin(), g->rowPtr.end() - 1);
-        for (int64_t e = 0; e < m; ++e) {
+        int64_t acc = 0;
+        for (int32_t v = 0; v < n; ++v) {
+            g->rowPtr[v] = (int32_t)std::min<int64_t>(acc, INT32_MAX);
+            for (int c = 0; c < NC; ++c) {
+                const int32_t x = cnt[c][v];
+                cnt[c][v] = (int32_t)std::min<int64_t>(acc, INT32_MAX);   // becomes the fill cursor
+                acc += x;
+            }
+        }
+        if (acc >= (int64_t)INT32_MAX) return SHD_PE_EINVAL;
+        g->rowPtr[n] = (int32_t)acc;
+    }
+    const int64_t nArcs = g->rowPtr[n];
+    g->col.resize(nArcs);
+    g->lat.resize(nArcs);
+    g->rel.resize(nArcs);
+    par_chunks(m, NC, m, [&](int c, int64_t e0, int64_t e1) {
+        std::vector<int32_t>& fill = cnt[c];
+        for (int64_t e = e0; e < e1; ++e) {
             const int32_t a = d->edgeFrom[e], b = d->edgeTo[e];
             if (a == b) continue;
             const double L = d->edgeLatency[e], R = 1.0 - d->edgePacketLoss[e];
@@ -117,21 +180,23 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
                 g->col[k] = a; g->lat[k] = L; g->rel[k] = R;
             }
         }
-    }
+    });
+    cnt.clear();
+    cnt.shrink_to_fit();
     int rc = sort_rows(n, g->rowPtr, g->col, g->lat, g->rel);
     if (rc) return rc;
 
-    g->outToIn.assign(nArcs, -1);
+    g->outToIn.resize(nArcs);
     if (g->directed) {
         // IN CSR sorted by source id
-        std::vector<int32_t> cnt(n + 1, 0);
-        for (int64_t a = 0; a < nArcs; ++a) cnt[g->col[a] + 1]++;
-        for (int32_t v = 0; v < n; ++v) cnt[v + 1] += cnt[v];
-        g->inPtr = cnt;
-        g->inCol.assign(nArcs, 0);
-        g->inLat.assign(nArcs, 0.0);
-        g->inRel.assign(nArcs, 0.0);
-        std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+        std::vector<int32_t> cntIn(n + 1, 0);
+        for (int64_t a = 0; a < nArcs; ++a) cntIn[g->col[a] + 1]++;
+        for (int32_t v = 0; v < n; ++v) cntIn[v + 1] += cntIn[v];
+        g->inPtr = cntIn;
+        g->inCol.resize(nArcs);
+        g->inLat.resize(nArcs);
+        g->inRel.resize(nArcs);
+        std::vector<int32_t> fill(cntIn.begin(), cntIn.end() - 1);
         for (int32_t u = 0; u < n; ++u) {               // rows visited in source order
             for (int32_t a = g->rowPtr[u]; a < g->rowPtr[u + 1]; ++a) {
                 const int32_t v = g->col[a];
@@ -141,13 +206,19 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
             }
         }
     } else {
-        for (int32_t u = 0; u < n; ++u) {
-            for (int32_t a = g->rowPtr[u]; a < g->rowPtr[u + 1]; ++a) {
-                const int64_t rev = g->findArc(g->col[a], u);
-                if (rev < 0) return SHD_PE_EINVAL;
-                g->outToIn[a] = (int32_t)rev;
+        // reverse arc of u->v: position of u in v's sorted row
+        std::vector<int> rcs(64, SHD_PE_OK);
+        par_chunks(n, 64, nArcs * 16, [&](int c, int64_t u0, int64_t u1) {
+            for (int64_t u = u0; u < u1; ++u) {
+                for (int32_t a = g->rowPtr[u]; a < g->rowPtr[u + 1]; ++a) {
+                    const int64_t rev = g->findArc(g->col[a], (int32_t)u);
+                    if (rev < 0) { rcs[c] = SHD_PE_EINVAL; return; }
+                    g->outToIn[a] = (int32_t)rev;
+                }
             }
-        }
+        });
+        for (int r : rcs)
+            if (r) return r;
     }
     // _topology_isComplete (topology.c:450-552): incident count (undirected
     // self-loop counted twice, then corrected by one) must reach vcount.
@@ -159,8 +230,16 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
         if (c < n) complete = false;
     }
     g->isComplete = complete;
+    // mean arc latency (bucket width): fixed 64-chunk partial sums added in
+    // order, so the value does not depend on the thread count
+    std::vector<double> part(64, 0.0);
+    par_chunks(nArcs, 64, nArcs, [&](int c, int64_t a0, int64_t a1) {
+        double s = 0.0;
+        for (int64_t a = a0; a < a1; ++a) s += g->lat[a];
+        part[c] = s;
+    });
     double sum = 0.0;
-    for (int64_t a = 0; a < nArcs; ++a) sum += g->lat[a];
+    for (double x : part) sum += x;
     g->meanArcLatency = nArcs ? sum / (double)nArcs : 1.0;
     return SHD_PE_OK;
 }

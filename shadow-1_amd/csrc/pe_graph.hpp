@@ -2,11 +2,28 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "shd_pathengine.h"
 
 namespace shdpe {
+
+// std::vector whose elements are default-initialised: the arc arrays of a
+// 2e8-edge topology are first touched by the (parallel) fill, not zeroed
+// serially first.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = DefaultInitAlloc<U>; };
+    using std::allocator<T>::allocator;
+    template <class U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using hvec = std::vector<T, DefaultInitAlloc<T>>;
 
 // CSR in igraph incidence order (ascending neighbour id) with self-loops
 // split out.  Built from the igraph edge list handed over the C-ABI.
@@ -15,12 +32,14 @@ struct HostGraph {
     int32_t directed = 0;
     int64_t nEdges = 0;
     // OUT arcs without self-loops
-    std::vector<int32_t> rowPtr, col;
-    std::vector<double> lat, rel;
+    std::vector<int32_t> rowPtr;
+    hvec<int32_t> col;
+    hvec<double> lat, rel;
     // IN arcs (directed only; undirected uses the OUT arrays)
-    std::vector<int32_t> inPtr, inCol;
-    std::vector<double> inLat, inRel;
-    std::vector<int32_t> outToIn;
+    std::vector<int32_t> inPtr;
+    hvec<int32_t> inCol;
+    hvec<double> inLat, inRel;
+    hvec<int32_t> outToIn;
     // vertex data
     std::vector<double> vrel;       // 1 - packetloss, 1.0 when absent/NaN
     std::vector<double> selfLat, selfRel;

@@ -100,7 +100,7 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab
                                          DistOf distOf, HopOf hopOf, const double* R,
                                          const int32_t* P, uint8_t extra, int tid, int NT) {
     const int T = (int)tab.T;
-    const size_t base = (size_t)r * (size_t)tab.T;
+    const size_t base = (size_t)(r - tab.rowStart) * (size_t)tab.T;
     double* __restrict__ oLat = tab.lat + base;
     double* __restrict__ oRel = tab.rel + base;
     int32_t* __restrict__ oHops = tab.hops + base;
@@ -423,26 +423,6 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
     c.hcap = hcap;
     c.R = sc.rel + slot;
     c.P = sc.pred + slot;
-
-    // ---- debug micro-probe: dependent global/LDS load latency, barrier cost
-    if (false) {
-        __syncthreads();
-        long long t0 = clock64();
-        int k = 0;
-        for (int it = 0; it < 32; ++it) k = g.col[(k + it * 97) % g.rowPtr[n]] & 1023;
-        long long t1 = clock64();
-        unsigned long long kk = k;
-        for (int it = 0; it < 32; ++it) kk = c.dist[(kk + it * 7) % n] & 1023;
-        long long t2 = clock64();
-        for (int it = 0; it < 32; ++it) __syncthreads();
-        long long t3 = clock64();
-        if (tid == 0) {
-            dbg[12] = (int)((t1 - t0) / 32);
-            dbg[13] = (int)((t2 - t1) / 32);
-            dbg[14] = (int)((t3 - t2) / 32);
-            dbg[15] = (int)(k + kk);
-        }
-    }
 
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
         const int r = rows[b];
@@ -1288,7 +1268,7 @@ __global__ __launch_bounds__(256) void k_direct_rows(DevGraph g0, DevTable tab0,
         if (a >= 0) { L = 0.0 + g.lat[a]; Rl = acc * g.rel[a]; h = 1; }
         else f |= F_NOEDGE;
     }
-    const size_t idx = (size_t)r * (size_t)tab.T + j;
+    const size_t idx = (size_t)(r - tab.rowStart) * (size_t)tab.T + j;
     tab.lat[idx] = L;
     tab.rel[idx] = Rl;
     tab.hops[idx] = h;
@@ -1344,11 +1324,11 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
 
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
-                       bool ldsIndex, void* stream) {
+                       bool ldsIndex, bool forceGlobalHeap, void* stream) {
     if (nRows <= 0) return;
     if (grid > nRows) grid = nRows;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (g.n <= EX_SOA_MAXN && !std::getenv("SHDPE_EXACT_AOS") && !std::getenv("SHDPE_EXACT_HC")) {
+    if (g.n <= EX_SOA_MAXN && !forceGlobalHeap) {
         const int sb = (int)(((size_t)16 * g.n + 15) & ~(size_t)15);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows_soa),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, sb);

@@ -111,9 +111,13 @@ static bool compute_source_paths(ShdTopology* t, int32_t s, int32_t d) {
                        t->rflags.data()))
         return false;
     t->rowsComputed++;
+    // topology.c:1815-1859: an empty igraph path (unreachable target) is
+    // skipped WITHOUT clearing isAllSuccess; only a failed fold
+    // (_topology_computePathProperties, e.g. a missing (s,s) self-loop) does
     bool allSuccess = true;
     for (size_t j = 0; j < T; ++j) {
-        if (t->rflags[j] & SHD_PE_F_FAILED) { allSuccess = false; continue; }
+        if (t->rflags[j] & SHD_PE_F_UNREACHABLE) continue;
+        if (t->rflags[j] & SHD_PE_F_NOEDGE) { allSuccess = false; continue; }
         store_path(t, false, s, t->attached[j], t->rlat[j], t->rrel[j]);
     }
     return allSuccess;

@@ -17,6 +17,8 @@ LIB_PATH = os.path.join(_PKG, "libshdpe.so")
 
 OK, EINVAL, ENOMEM, ENODEV, EUNREACHABLE, ENOSELFLOOP, EMULTI, EHIP, ENOTATTACHED, ENOEDGE = (
     0, -1, -2, -3, -4, -5, -6, -7, -8, -9)
+ENOTOWNED, ETOOBIG, ECOMM = -10, -11, -12
+DEBUG_ENV, DEBUG_COUNTERS = 0x1, 0x2
 F_UNREACHABLE, F_NOEDGE, F_ZEROLAT, F_DIRECT, F_EXACT = 0x01, 0x02, 0x04, 0x08, 0x10
 F_FAILED = F_UNREACHABLE | F_NOEDGE
 
@@ -25,7 +27,8 @@ EXPORTS = [
     "shd_pe_is_complete", "shd_pe_num_attached", "shd_pe_attached", "shd_pe_compute_all",
     "shd_pe_compute_rows", "shd_pe_compute_positions", "shd_pe_get_row", "shd_pe_get_rows",
     "shd_pe_copy_rows_device", "shd_pe_synchronize", "shd_pe_get_stats", "shd_pe_reset_stats",
-    "shd_pe_stream_bandwidth",
+    "shd_pe_stream_bandwidth", "shd_pe_num_shards", "shd_pe_shard_bounds", "shd_pe_plan_shards", "shd_pe_owned_range",
+    "shd_pe_gather", "shd_pe_comm_unique_id", "shd_pe_comm_init",
     "shd_pe_direct_path", "shd_pe_self_path", "shd_pe_adjacent", "shd_topology_new",
     "shd_topology_free", "shd_topology_get_latency", "shd_topology_get_reliability",
     "shd_topology_is_routable", "shd_topology_increment_path_packet_counter",
@@ -43,7 +46,9 @@ class GraphDesc(C.Structure):
 
 class Options(C.Structure):
     _fields_ = [("device", C.c_int32), ("batchRows", C.c_int32), ("delta", C.c_double),
-                ("storePred", C.c_int32), ("forceMode", C.c_int32)]
+                ("storePred", C.c_int32), ("forceMode", C.c_int32), ("nDevices", C.c_int32),
+                ("devices", C.c_void_p), ("shardIndex", C.c_int32), ("shardCount", C.c_int32),
+                ("debugFlags", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -56,7 +61,8 @@ class Stats(C.Structure):
                 ("nArcs", C.c_int64), ("nAttached", C.c_int32), ("deltaUsed", C.c_double),
                 ("msDenseKernel", C.c_double), ("launchesDense", C.c_int64),
                 ("denseSweeps", C.c_int64), ("denseFlops", C.c_double),
-                ("batched", C.c_int32), ("batchLanes", C.c_int32)]
+                ("batched", C.c_int32), ("batchLanes", C.c_int32), ("nShards", C.c_int32),
+                ("msGather", C.c_double)]
 
 
 class EngineError(RuntimeError):
@@ -96,6 +102,13 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_get_stats": (C.c_int, [vp, vp]),
         "shd_pe_reset_stats": (C.c_int, [vp]),
         "shd_pe_stream_bandwidth": (C.c_int, [vp, i64, i32, vp]),
+        "shd_pe_num_shards": (i32, [vp]),
+        "shd_pe_shard_bounds": (C.c_int, [vp, vp]),
+        "shd_pe_plan_shards": (C.c_int, [i32, i32, i32, vp]),
+        "shd_pe_owned_range": (C.c_int, [vp, vp, vp]),
+        "shd_pe_gather": (C.c_int, [vp]),
+        "shd_pe_comm_unique_id": (C.c_int, [vp, i32]),
+        "shd_pe_comm_init": (C.c_int, [vp, vp, i32]),
         "shd_pe_direct_path": (C.c_int, [vp, i32, i32, vp, vp]),
         "shd_pe_self_path": (C.c_int, [vp, i32, vp, vp]),
         "shd_pe_adjacent": (C.c_int, [vp, i32, i32]),
@@ -122,6 +135,15 @@ def load_library(path: str = LIB_PATH):
     return lib
 
 
+def plan_shards(T: int, G: int, unit: int = 1) -> np.ndarray:
+    """shd_pe_plan_shards: the engine's row-shard bounds (host only)."""
+    b = np.empty(G + 1, np.int32)
+    rc = load_library().shd_pe_plan_shards(int(T), int(G), int(unit), _p(b))
+    if rc:
+        raise EngineError(rc, "shd_pe_plan_shards")
+    return b
+
+
 def strerror(code: int) -> str:
     return load_library().shd_pe_strerror(int(code)).decode()
 
@@ -134,7 +156,11 @@ class Engine:
     """One path engine on one gfx950 device (shd_pe_create)."""
 
     def __init__(self, top, attached, device: int = 0, delta: float = 0.0,
-                 store_pred: bool = True, force_mode: int = 0):
+                 store_pred: bool = True, force_mode: int = 0, devices=None,
+                 shard_index: int = 0, shard_count: int = 1, debug_flags: int = 0):
+        """devices: list of HIP ordinals, one row shard each (repeats = logical
+        shards on one device); shard_index/shard_count: this process's engine
+        among several (multi-process row shards)."""
         lib = load_library()
         self._lib = lib
         self.top = top
@@ -144,6 +170,10 @@ class Engine:
         o = Options()
         lib.shd_pe_default_options(C.byref(o))
         o.device, o.delta, o.storePred, o.forceMode = device, delta, int(store_pred), force_mode
+        o.shardIndex, o.shardCount, o.debugFlags = shard_index, shard_count, debug_flags
+        if devices is not None:
+            self._devs = np.ascontiguousarray(devices, dtype=np.int32)
+            o.nDevices, o.devices = int(self._devs.shape[0]), _p(self._devs)
         att = np.ascontiguousarray(attached, dtype=np.int32)
         h = C.c_void_p()
         rc = lib.shd_pe_create(C.byref(d), _p(att), att.shape[0], C.byref(o), C.byref(h))
@@ -155,6 +185,29 @@ class Engine:
         self.attached = np.empty(T, np.int32)
         lib.shd_pe_attached(h, _p(self.attached))
         self.T = T
+        st, cnt = C.c_int32(), C.c_int32()
+        lib.shd_pe_owned_range(h, C.byref(st), C.byref(cnt))
+        self.owned = (st.value, cnt.value)
+
+    def shard_bounds(self):
+        G = self._lib.shd_pe_num_shards(self.h)
+        b = np.empty(G + 1, np.int32)
+        self._chk(self._lib.shd_pe_shard_bounds(self.h, _p(b)), "shd_pe_shard_bounds")
+        return b
+
+    def gather(self):
+        self._chk(self._lib.shd_pe_gather(self.h), "shd_pe_gather")
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        rc = load_library().shd_pe_comm_unique_id(buf, 128)
+        if rc:
+            raise EngineError(rc, "shd_pe_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, uid: bytes):
+        self._chk(self._lib.shd_pe_comm_init(self.h, uid, len(uid)), "shd_pe_comm_init")
 
     def close(self):
         if getattr(self, "h", None):

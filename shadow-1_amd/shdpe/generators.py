@@ -105,14 +105,25 @@ def power_law(n: int = 100_000, m: int = 3, seed: int = 4, quantum: float = 0.0)
     return Topology(n=n, directed=False, src=np.concatenate([a, np.arange(n)]),
                     dst=np.concatenate([b, np.arange(n)]), latency=latency,
                     loss=np.concatenate([loss, self_loss]), vloss=np.zeros(n),
-                    name=f"ba{n}_m{m}_s{seed}")
+                    name=f"ba{n}_m{m}_s{seed}" + (f"_q{quantum}" if quantum else ""))
+
+
+def _triu_pairs(n: int):
+    """np.triu_indices(n, k=1) (row-major pairs i < j) as int32, without the
+    n x n mask (C3: 2e8 pairs)."""
+    cnt = np.arange(n - 1, 0, -1, dtype=np.int64)              # row i has n-1-i pairs
+    iu = np.repeat(np.arange(n - 1, dtype=np.int32), cnt)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    ju = np.arange(iu.shape[0], dtype=np.int64)
+    ju -= np.repeat(start - np.arange(1, n, dtype=np.int64), cnt)
+    return iu, ju.astype(np.int32)
 
 
 def dense(n: int = 20_000, seed: int = 3, drop_edge: bool = False) -> Topology:
     """Complete graph + self-loops; ``drop_edge`` removes
     one non-loop edge so ``_topology_isComplete`` is FALSE (C3b)."""
     rng = np.random.default_rng(seed)
-    iu, ju = np.triu_indices(n, k=1)
+    iu, ju = _triu_pairs(n)
     lat = np.clip(rng.lognormal(np.log(60.0), 0.8, size=iu.shape[0]), 1.0, 2000.0)
     if drop_edge:
         k = int(rng.integers(iu.shape[0]))
@@ -191,7 +202,11 @@ def sample_attached(n: int, k: int, seed: int) -> np.ndarray:
 
 CONFIGS = {
     "c2": dict(desc="RGG n=10k, all 10k sources (BASELINE.json configs[1])"),
-    "c4": dict(desc="BA n=100k m=3, 16,384 attached (configs[3])"),
+    "c4": dict(desc="BA n=100k m=3, 16,384 attached (configs[3], north_star target)"),
+    "c4q": dict(desc="C4 with latencies rounded to 0.005 ms (tie stress, SURVEY.md 8d)"),
+    "c2q": dict(desc="C2 with latencies rounded to 0.005 ms (tie stress, SURVEY.md 8d)"),
+    "c3a": dict(desc="dense n=20k complete (configs[2], direct rows)"),
+    "c3b": dict(desc="dense n=20k minus one edge (configs[2], min-plus)"),
     "c5": dict(desc="BA n=250k m=2, 65,536 attached (configs[4])"),
 }
 
@@ -203,7 +218,8 @@ def make_config(name: str):
     c1m  shipped topology minus one edge (Dijkstra semantics, tie stress)
     c2   RGG 10k, all sources        c2q  same, latencies rounded to 0.005
     c3a  dense 20k complete           c3b  dense 20k minus one edge
-    c4   BA 100k, 16,384 attached     c5   BA 250k, 65,536 attached
+    c4   BA 100k, 16,384 attached     c4q  same, latencies rounded to 0.005
+    c5   BA 250k, 65,536 attached
     """
     if name in ("c1", "c1m"):
         import os
@@ -224,8 +240,8 @@ def make_config(name: str):
     if name == "c2q":
         top = rgg(10_000, seed=1, quantum=0.005)
         return top, np.arange(top.n, dtype=np.int32)
-    if name == "c4":
-        top = power_law(100_000, m=3, seed=4)
+    if name in ("c4", "c4q"):
+        top = power_law(100_000, m=3, seed=4, quantum=0.005 if name == "c4q" else 0.0)
         return top, sample_attached(top.n, 16_384, seed=5)
     if name == "c5":
         top = power_law(250_000, m=2, seed=6)

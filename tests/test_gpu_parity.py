@@ -39,8 +39,8 @@ def _assert_rows_equal(got, exp, ctx=""):
         assert np.array_equal(got["pred"][ok], exp["pred"][ok]), ctx
 
 
-def _check_engine(E, oracle_mod, top, att, sources=None, force=0):
-    eng = E.Engine(top, att, force_mode=force)
+def _check_engine(E, oracle_mod, top, att, sources=None, force=0, debug_flags=0):
+    eng = E.Engine(top, att, force_mode=force, debug_flags=debug_flags)
     og = oracle_mod.OracleGraph(top)
     srcs = eng.attached if sources is None else np.asarray(sources, np.int32)
     eng.compute_rows(srcs)
@@ -104,7 +104,7 @@ def test_exact_kernel_heap_tail_in_global(E, oracle_mod, monkeypatch):
     2-way heap lives in the global slot (the split the large graphs use)."""
     monkeypatch.setenv("SHDPE_EXACT_HC", "5")
     top = G.random_sparse(300, 5, seed=11, quantum=2.0)
-    st = _check_engine(E, oracle_mod, top, np.arange(0, 300, 3), force=3)
+    st = _check_engine(E, oracle_mod, top, np.arange(0, 300, 3), force=3, debug_flags=E.DEBUG_ENV)
     assert st["rowsExact"] == 100
 
 

@@ -115,36 +115,42 @@ def test_config_c2_shape():
 
 
 def _gloo_worker(rank, world, port, q):
+    """Rank `rank` of a world-2 job: its rows come from the engine's own shard
+    plan (shd_pe_plan_shards, the function shd_pe_create uses); the blocks
+    are assembled the way shd_pe_gather does (one broadcast per shard, each
+    landing at its row offset).  No GPU here, so the oracle produces the
+    shard's rows -- the GPU engine's sharded tables are checked byte for byte
+    in tests/test_gpu_parity.py::test_sharded_engine_*."""
     import torch.distributed as dist
     sys.path[:0] = [os.path.join(ROOT, "shadow-1_amd"), os.path.join(ROOT, "oracle"), ROOT]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
 
-    import bench
     import oracle as O
+    from shdpe.engine import plan_shards
     top = G.random_sparse(120, 4, seed=5)
     att = np.arange(0, 120, 1, dtype=np.int32)
     T = att.shape[0]
-    start, count = bench.shard(T, rank, world)
+    bounds = plan_shards(T, world, unit=16)
+    start, count = int(bounds[rank]), int(bounds[rank + 1] - bounds[rank])
     og = O.OracleGraph(top)
-    # the oracle stands in for the engine here (CPU test of the shard logic)
+    full = torch.zeros(T * T, dtype=torch.float64)
     mine = og.rows(att[start:start + count], att)["lat"]
-    blk = (T + world - 1) // world
-    buf = torch.zeros(blk * T, dtype=torch.float64)
-    buf[: count * T] = torch.from_numpy(mine.ravel())
-    full = torch.empty(world * blk * T, dtype=torch.float64)
-    dist.all_gather_into_tensor(full, buf)
-    table = np.concatenate([full[r * blk * T: r * blk * T + bench.shard(T, r, world)[1] * T].numpy()
-                            for r in range(world)]).reshape(T, T)
+    full[start * T:(start + count) * T] = torch.from_numpy(mine.ravel())
+    for g in range(world):                 # allgatherv = per-shard broadcasts
+        lo, hi = int(bounds[g]) * T, int(bounds[g + 1]) * T
+        blk = full[lo:hi].clone()
+        dist.broadcast(blk, src=g)
+        full[lo:hi] = blk
     if rank == 0:
         ref = og.rows(att, att)["lat"]
-        q.put(bool(np.array_equal(table.view(np.int64), ref.view(np.int64))))
+        q.put(bool(np.array_equal(full.numpy().reshape(T, T).view(np.int64), ref.view(np.int64))))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_shard_and_allgather_world2_gloo(oracle_mod):
+def test_shard_and_allgather_world2_gloo(oracle_mod, lib):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -158,13 +164,15 @@ def test_shard_and_allgather_world2_gloo(oracle_mod):
     assert ok
 
 
-def test_shard_partition():
-    import bench
-    for T in (1, 7, 10_000, 65_536):
+def test_shard_plan(lib):
+    """shd_pe_plan_shards: contiguous, covering, unit-aligned, balanced."""
+    from shdpe.engine import plan_shards
+    for T in (1, 7, 100, 10_000, 16_384, 65_536):
         for world in (1, 2, 3, 8):
-            parts = [bench.shard(T, r, world) for r in range(world)]
-            assert parts[0][0] == 0
-            for (s0, c0), (s1, _) in zip(parts, parts[1:]):
-                assert s0 + c0 == s1
-            assert sum(c for _, c in parts) == T
-            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+            for unit in (1, 16):
+                b = plan_shards(T, world, unit)
+                assert b[0] == 0 and b[-1] == T and np.all(np.diff(b) >= 0)
+                assert np.all(b[:-1] % unit == 0)
+                units = np.diff((b + unit - 1) // unit)
+                assert units.max() - units.min() <= 1
+    assert list(plan_shards(16_384, 8, 16)) == [2048 * g for g in range(9)]

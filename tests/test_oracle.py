@@ -179,6 +179,28 @@ def test_unreachable_directed(oracle_mod):
     assert r["flags"][1] == 0 and r["lat"][1] == 1.0
 
 
+def test_unreachable_target_keeps_row_success(oracle_mod):
+    """topology.c:1815-1859: an empty igraph path (unreachable target) is
+    skipped WITHOUT clearing isAllSuccess, so the lookup that triggered the
+    row still succeeds; only a failed fold (missing (s,s) loop, :1857) fails
+    it.  Directed 0 -> 1 -> 2 with 2 -> 1 only: from 1, vertex 0 is
+    unreachable but (1,2) is found."""
+    src = np.array([0, 1, 2, 0, 1, 2])
+    dst = np.array([1, 2, 1, 0, 1, 2])
+    top = Topology(3, True, src, dst, np.array([2.0, 3.0, 4.0, 1.0, 1.0, 1.0]), np.zeros(6))
+    og = _og(oracle_mod, top)
+    T = oracle_mod.OracleTopology(og, np.arange(3, dtype=np.int32))
+    assert T.get_latency(1, 2) == 3.0              # row 1 has unreachable target 0
+    assert T.rows_computed == 1
+    assert T.cached(1, 0) is None                   # not stored (:1815)
+    assert T.get_latency(1, 0) == -1.0              # the unreachable pair itself fails
+    # a missing self-loop fails the fold of (s,s) -> the whole lookup fails (:1857)
+    top2 = Topology(3, True, src[:5], dst[:5], np.array([2.0, 3.0, 4.0, 1.0, 1.0]), np.zeros(5))
+    T2 = oracle_mod.OracleTopology(_og(oracle_mod, top2), np.arange(3, dtype=np.int32))
+    assert T2.get_latency(2, 1) == -1.0            # row 2: (2,2) has no edge
+    assert T2.cached(2, 1) is not None              # ... though (2,1) itself was stored
+
+
 @pytest.mark.parametrize("name", ["rows_shipped_minus1", "rows_rand_tiefree", "rows_rand_quantized",
                                   "rows_rand_directed", "rows_rand_vloss", "rows_rgg2000",
                                   "rows_rgg2000_q"])
@@ -258,3 +280,10 @@ def test_graphml_reader_doc_example():
     top = read_graphml(xml)
     assert top.n == 1 and top.m == 1 and not top.directed
     assert top.latency[0] == 50.0 and top.loss[0] == 0.001 and top.vloss[0] == 0.0
+
+
+@pytest.mark.parametrize("m,nodes", [(1000, 7), (50_000, 300), (200_000, 20_000)])
+def test_vector_order_counting_form_matches_igraph_form(oracle_mod, m, nodes):
+    """The oracle sorts huge edge lists (C3) with counting sorts; the order
+    must be igraph_vector_order's exactly, parallel edges newest-first."""
+    assert oracle_mod.lib().orc_selftest_vector_order(m, nodes, 12345) == 1
