@@ -120,7 +120,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                                                            BatchScratch bs,
                                                            const int32_t* __restrict__ batchRows,
                                                            int32_t nBatches, uint8_t* rowAmbig,
-                                                           double delta, int32_t* dbg) {
+                                                           double delta, int32_t* dbg, int kflags) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
@@ -313,8 +313,12 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                             if (x >= 0) {
                                 const unsigned long long nb = d2b(b2d(dub[v]) + ws[v][k]);
                                 if (nb < dx[v][k]) {
-                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                    if (kflags & 1)
+                                        __hip_atomic_store(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    else
+                                        __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP);
                                     imp = true;
                                 }
                             }
@@ -739,7 +743,7 @@ static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
     hipLaunchKernelGGL(k_batch_rows<LB>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
-                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg);
+                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, cfg.kflags);
 }
 
 int batch_lds_bytes(int n) {

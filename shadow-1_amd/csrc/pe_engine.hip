@@ -144,6 +144,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_LB", t.batchLB);
     gi("SHDPE_BATCH_THREADS", t.batchThreads);
     gi("SHDPE_BATCH_GRID", t.batchGrid);
+    gi("SHDPE_BATCH_KFLAGS", t.batchKflags);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -276,6 +277,7 @@ static int configure(ShdPe* pe, Shard* sh) {
     if (tu.batchGrid > 0 && tu.batchGrid < b.grid) b.grid = tu.batchGrid;
     b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
     if (!(b.delta > 0)) b.delta = 1.0;
+    b.kflags = tu.batchKflags;
     sh->bcfg = b;
     sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
     sh->stats.batched = pe->batched ? 1 : 0;
