@@ -152,6 +152,12 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
     unsigned long long* JH = reinterpret_cast<unsigned long long*>(X);   // 2 SE words
     int2* LV = reinterpret_cast<int2*>(X + 2 * SE);                     // 2 SE words
     int32_t* Q = as_global(bs.queue + slot * NS);
+    // per-lane pending masks (kflags & 2): bit l of PM[v] = lane l of v changed
+    // since it was last relaxed; without them every lane below the bound of a
+    // pending vertex is re-relaxed
+    const bool masks = (kflags & 2) != 0;
+    uint32_t* const PM0 = as_global(bs.pm + slot * 2 * NS);
+    uint32_t* const PM1 = PM0 + NS;
 
     for (int b = blockIdx.x; b < nBatches; b += gridDim.x) {
         const int row = batchRows[(size_t)b * LB + l];
@@ -162,6 +168,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             const size_t cnt2 = NE / 2;
             const ulonglong2 inf2 = make_ulonglong2(INF_BITS, INF_BITS);
             for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
+            if (masks)
+                for (size_t i = tid; i < NS; i += NT) { PM0[i] = 0u; PM1[i] = 0u; }
             for (int w = tid; w < nwp; w += NT) { any0[w] = 0u; any1[w] = 0u; }
             if (tid == 0) {
                 ctl->qtail = 0;
@@ -180,6 +188,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             D[(size_t)src * LB + l] = d2b(0.0);
             R[(size_t)src * LB + l] = 1.0;
             atomicOr(&any0[src >> 5], 1u << (src & 31));
+            if (masks) atomicOr(&PM0[src], 1u << l);
         }
         fence_wg();
         __syncthreads();
@@ -210,6 +219,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         for (;;) {
             uint32_t* const anyC = par ? any1 : any0;
             uint32_t* const anyN = par ? any0 : any1;
+            uint32_t* const PMc = par ? PM1 : PM0;
+            uint32_t* const PMn = par ? PM0 : PM1;
             // candidates = vertices with a pending bit (cur set, consumed)
             for (int w = tid; w < nw; w += NT) {
                 uint32_t bits = anyC[w];
@@ -245,6 +256,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             }
             for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
                 int u[BV], a0[BV], a1[BV];
+                uint32_t pmk[BV];
                 unsigned long long db[BV], dub[BV];
 #pragma unroll
                 for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? nq[v] : -1;
@@ -259,6 +271,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                     const int uc = u[v] >= 0 ? u[v] : 0;
                     const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
                     const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
+                    pmk[v] = masks ? ld_wg(&PMc[uc]) : LBMASK;
                     db[v] = u[v] >= 0 ? d0 : INF_BITS;
                     a0[v] = u[v] >= 0 ? r0 : 0;
                     a1[v] = u[v] >= 0 ? r1 : 0;
@@ -266,10 +279,15 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                 int maxd = 0;
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    const bool act = b2d(db[v]) < bound;
-                    const bool defer = !act && db[v] != INF_BITS;
+                    const bool pend = (pmk[v] >> l) & 1u;
+                    const bool act = pend && b2d(db[v]) < bound;
+                    const bool defer = pend && !act && db[v] != INF_BITS;
                     const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
                     const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
+                    if (masks && l == 0 && u[v] >= 0) {
+                        __hip_atomic_store(&PMc[u[v]], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (dmask) atomicOr(&PMn[u[v]], dmask);
+                    }
                     if (l == 0 && dmask) atomicOr(&anyN[u[v] >> 5], 1u << (u[v] & 31));
                     if (defer) myMin = db[v] < myMin ? db[v] : myMin;
                     dub[v] = act ? db[v] : INF_BITS;
@@ -322,8 +340,10 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                                     imp = true;
                                 }
                             }
-                            if (__ballot(imp) >> gbase & LBMASK && l == 0) {
+                            const uint32_t imask = (uint32_t)(__ballot(imp) >> gbase) & LBMASK;
+                            if (imask && l == 0) {
                                 atomicOr(&anyN[x >> 5], 1u << (x & 31));
+                                if (masks) atomicOr(&PMn[x], imask);
                                 myAct = 1;
                             }
                         }
@@ -465,7 +485,10 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                         viol = 1;
                     }
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
-                    if (bm && l == 0) atomicOr(&anyC[vv >> 5], 1u << (vv & 31));
+                    if (bm && l == 0) {
+                        atomicOr(&anyC[vv >> 5], 1u << (vv & 31));
+                        if (masks) atomicOr(&(par ? PM1 : PM0)[vv], bm);
+                    }
                     const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
                     if (!root[v] && dvb[v] != INF_BITS && cnt[v] != 1) amb = true;
                     P[e] = tree ? ba[v] : -1;

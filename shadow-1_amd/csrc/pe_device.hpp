@@ -74,7 +74,7 @@ struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0, exactAos = 0;
-    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchKflags = 0;
+    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchKflags = 0, batchOrder = 0;
     double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
@@ -111,6 +111,7 @@ struct BatchScratch {
     int32_t* H;              // [slot][nStride][LB] hop label
     int32_t* P;              // [slot][nStride][LB] chosen IN-arc, -1 none
     int32_t* X;              // [slot][4][nStride*LB] pointer-jumping / level lists
+    uint32_t* pm;            // [slot][2][nStride] pending lane masks (cur/next)
     int32_t* queue;          // [slot][nStride] phase candidate list
     int64_t nStride;         // >= n, multiple of 64
 };
@@ -121,7 +122,8 @@ struct BatchLaunch {
     int32_t grid;            // resident workgroups (= scratch slots)
     int32_t ldsBytes;
     double delta;            // bucket width
-    int32_t kflags;          // experiment bits (tuning): 1 plain stores in the relax phase
+    int32_t kflags;          // variant bits: 1 plain stores in the relax phase (experiment),
+                             // 2 per-lane pending masks
 };
 
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)

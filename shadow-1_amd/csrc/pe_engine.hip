@@ -28,6 +28,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <queue>
 #include <thread>
 #include <vector>
 
@@ -145,6 +146,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_THREADS", t.batchThreads);
     gi("SHDPE_BATCH_GRID", t.batchGrid);
     gi("SHDPE_BATCH_KFLAGS", t.batchKflags);
+    gi("SHDPE_BATCH_ORDER", t.batchOrder);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -285,28 +287,67 @@ static int configure(ShdPe* pe, Shard* sh) {
     return SHD_PE_OK;
 }
 
-// BFS visit rank of every table position (components in vertex order):
-// batches of nearby sources share their delta-stepping frontiers.
+// Batch order of the table positions: sources of one batch should have
+// similar distance profiles so their delta-stepping frontiers coincide.
+//   order 0: BFS visit rank (components in vertex order);
+//   order 1: nearest-hub cells -- a multi-source Dijkstra from the K
+//            highest-degree vertices gives every vertex its closest hub;
+//            sources sort by (hub, distance to it), so a batch holds
+//            sources that reach the rest of the graph through one hub.
+// Scheduling only: results never depend on it.
 static void compute_ranks(ShdPe* pe) {
     const HostGraph& g = pe->hg;
     std::vector<int32_t> order;
     order.reserve(g.n);
-    std::vector<uint8_t> seen(g.n, 0);
-    for (int32_t r = 0; r < g.n; ++r) {
-        if (seen[r]) continue;
-        seen[r] = 1;
-        size_t head = order.size();
-        order.push_back(r);
-        while (head < order.size()) {
-            const int32_t u = order[head++];
+    if (pe->tu.batchOrder == 1) {
+        const int32_t K = (int32_t)std::max<int64_t>(1, std::min<int64_t>(256, g.n / 400));
+        std::vector<int32_t> byDeg(g.n);
+        for (int32_t v = 0; v < g.n; ++v) byDeg[v] = v;
+        std::stable_sort(byDeg.begin(), byDeg.end(), [&](int32_t a, int32_t b) {
+            return g.rowPtr[a + 1] - g.rowPtr[a] > g.rowPtr[b + 1] - g.rowPtr[b];
+        });
+        std::vector<double> dist(g.n, INFINITY);
+        std::vector<int32_t> owner(g.n, INT32_MAX);
+        typedef std::pair<double, int32_t> QE;
+        std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
+        for (int32_t k = 0; k < K; ++k) { dist[byDeg[k]] = 0.0; owner[byDeg[k]] = k; q.push({0.0, byDeg[k]}); }
+        while (!q.empty()) {
+            const QE top = q.top();
+            q.pop();
+            const int32_t u = top.second;
+            if (top.first > dist[u]) continue;
             for (int32_t a = g.rowPtr[u]; a < g.rowPtr[u + 1]; ++a) {
                 const int32_t v = g.col[a];
-                if (!seen[v]) { seen[v] = 1; order.push_back(v); }
+                const double nd = dist[u] + g.lat[a];
+                if (nd < dist[v] || (nd == dist[v] && owner[u] < owner[v])) {
+                    dist[v] = nd;
+                    owner[v] = owner[u];
+                    q.push({nd, v});
+                }
             }
-            if (g.directed) {
-                for (int32_t a = g.inPtr[u]; a < g.inPtr[u + 1]; ++a) {
-                    const int32_t v = g.inCol[a];
+        }
+        for (int32_t v = 0; v < g.n; ++v) order.push_back(v);
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+            return owner[a] != owner[b] ? owner[a] < owner[b] : dist[a] < dist[b];
+        });
+    } else {
+        std::vector<uint8_t> seen(g.n, 0);
+        for (int32_t r = 0; r < g.n; ++r) {
+            if (seen[r]) continue;
+            seen[r] = 1;
+            size_t head = order.size();
+            order.push_back(r);
+            while (head < order.size()) {
+                const int32_t u = order[head++];
+                for (int32_t a = g.rowPtr[u]; a < g.rowPtr[u + 1]; ++a) {
+                    const int32_t v = g.col[a];
                     if (!seen[v]) { seen[v] = 1; order.push_back(v); }
+                }
+                if (g.directed) {
+                    for (int32_t a = g.inPtr[u]; a < g.inPtr[u + 1]; ++a) {
+                        const int32_t v = g.inCol[a];
+                        if (!seen[v]) { seen[v] = 1; order.push_back(v); }
+                    }
                 }
             }
         }
@@ -576,7 +617,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     if (sh->batchReady) return SHD_PE_OK;
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     const size_t LB = (size_t)sh->bcfg.lb;
-    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4;
+    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4 * 3;
     // scratch budget (default 64 GiB): fewer resident batches on huge graphs
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
@@ -584,11 +625,11 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     size_t slots = std::min<size_t>({(size_t)sh->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
     sh->bcfg.grid = (int32_t)slots;
     int rc;
-    void *D, *R, *H, *P, *X, *q, *rows, *amb;
+    void *D, *R, *H, *P, *X, *q, *pm, *rows, *amb;
     if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &X, slots * NS * LB * 16)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
-        (rc = dev_alloc(sh, &q, slots * NS * 4)) ||
+        (rc = dev_alloc(sh, &q, slots * NS * 4)) || (rc = dev_alloc(sh, &pm, slots * NS * 2 * 4)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
         (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)))
         return rc;
@@ -598,6 +639,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.P = (int32_t*)P;
     sh->bsc.X = (int32_t*)X;
     sh->bsc.queue = (int32_t*)q;
+    sh->bsc.pm = (uint32_t*)pm;
     sh->bsc.nStride = (int64_t)NS;
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
