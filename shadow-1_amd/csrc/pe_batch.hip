@@ -140,6 +140,10 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
     uint32_t* const any1 = any0 + nwp;
     int32_t* const hist = reinterpret_cast<int32_t*>(any1 + nwp);   // [LMAX + 2]
     int32_t* const cur = hist + (LMAX + 4);                           // [LMAX + 2]
+    // pull relax (kflags & 4): frontier bits F and touched bits of the phase
+    const bool pull = (kflags & 4) != 0;
+    uint32_t* const fbits = reinterpret_cast<uint32_t*>(cur + (LMAX + 4));
+    uint32_t* const tbits = fbits + nwp;
 
     const size_t slot = blockIdx.x;
     const size_t NS = (size_t)bs.nStride;
@@ -171,6 +175,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             if (masks)
                 for (size_t i = tid; i < NS; i += NT) { PM0[i] = 0u; PM1[i] = 0u; }
             for (int w = tid; w < nwp; w += NT) { any0[w] = 0u; any1[w] = 0u; }
+            if (pull)
+                for (int w = tid; w < nwp; w += NT) { fbits[w] = 0u; tbits[w] = 0u; }
             if (tid == 0) {
                 ctl->qtail = 0;
                 ctl->active = 0;
@@ -224,6 +230,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             // candidates = vertices with a pending bit (cur set, consumed)
             for (int w = tid; w < nw; w += NT) {
                 uint32_t bits = anyC[w];
+                if (pull) fbits[w] = bits;
                 if (bits) {
                     anyC[w] = 0u;
                     int pos = atomicAdd(&ctl->qtail, __popc(bits));
@@ -245,6 +252,137 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             unsigned long long myMin = INF_BITS;
             int myAct = 0;
             const long long tg0 = dbg ? (long long)clock64() : 0;
+            if (pull) {
+                // ---- pull relax: no atomics on dist, one writer per vertex ----
+                // (B) frontier: lanes below the bound are active; deferred
+                // lanes keep u pending; u without active lanes leaves F; the
+                // out-neighbours of active u are marked touched
+                for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
+                    int u[BV], a0[BV], a1[BV];
+                    unsigned long long db[BV];
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        const int uu = i0 + v < qn ? ld_wg(&Q[i0 + v]) : -1;
+                        const int uc = uu >= 0 ? uu : 0;
+                        const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                        const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
+                        u[v] = uu;
+                        db[v] = uu >= 0 ? d0 : INF_BITS;
+                        a0[v] = uu >= 0 ? r0 : 0;
+                        a1[v] = uu >= 0 ? r1 : 0;
+                    }
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        if (u[v] < 0) continue;
+                        const bool act = b2d(db[v]) < bound;
+                        const bool defer = !act && db[v] != INF_BITS;
+                        const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
+                        const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
+                        if (l == 0 && dmask) atomicOr(&anyN[u[v] >> 5], 1u << (u[v] & 31));
+                        if (defer) myMin = db[v] < myMin ? db[v] : myMin;
+                        if (!amask) {
+                            if (l == 0) atomicAnd(&fbits[u[v] >> 5], ~(1u << (u[v] & 31)));
+                            continue;
+                        }
+                        ++procs;
+                        lanesAct += __popc(amask);
+                        for (int a = a0[v] + l; a < a1[v]; a += LB) {
+                            const int x = g.col[a];
+                            atomicOr(&tbits[x >> 5], 1u << (x & 31));
+                        }
+                    }
+                }
+                __syncthreads();
+                // (C) touched vertices -> queue (reuses Q: the frontier list
+                // is not needed any more)
+                if (tid == 0) ctl->qtail = 0;
+                __syncthreads();
+                for (int w = tid; w < nw; w += NT) {
+                    uint32_t bits = tbits[w];
+                    if (bits) {
+                        tbits[w] = 0u;
+                        int pos = atomicAdd(&ctl->qtail, __popc(bits));
+                        while (bits) {
+                            const int bb = __ffs(bits) - 1;
+                            bits &= bits - 1;
+                            Q[pos++] = (w << 5) + bb;
+                        }
+                    }
+                }
+                fence_wg();
+                __syncthreads();
+                const int tn = ctl->qtail;
+                // (D) every touched x takes min over frontier in-neighbours u
+                // of dist[u] + w (left fold) for u's active lanes; one plain
+                // store by the only writer of x in this phase
+                for (int i0 = gid * BV; i0 < tn; i0 += NG * BV) {
+                    int x[BV], a0[BV], a1[BV];
+                    unsigned long long dxv[BV], best[BV];
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        const int xx = i0 + v < tn ? ld_wg(&Q[i0 + v]) : -1;
+                        const int xc = xx >= 0 ? xx : 0;
+                        const unsigned long long d0 = ld_wg(&D[(size_t)xc * LB + l]);
+                        const int r0 = undirected ? g.rowPtr[xc] : g.inPtr[xc];
+                        const int r1 = undirected ? g.rowPtr[xc + 1] : g.inPtr[xc + 1];
+                        x[v] = xx;
+                        dxv[v] = d0;
+                        best[v] = INF_BITS;
+                        a0[v] = xx >= 0 ? r0 : 0;
+                        a1[v] = xx >= 0 ? r1 : 0;
+                    }
+                    int maxd = 0;
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) maxd = max(maxd, a1[v] - a0[v]);
+                    for (int t = 0; t < maxd; t += BK) {
+                        int us[BV][BK];
+                        double ws[BV][BK];
+                        unsigned long long du[BV][BK];
+#pragma unroll
+                        for (int v = 0; v < BV; ++v)
+#pragma unroll
+                            for (int k = 0; k < BK; ++k) {
+                                const int a = a0[v] + t + k;
+                                const bool ok = a < a1[v];
+                                const int ac = ok ? a : 0;
+                                int c;
+                                double w;
+                                if (undirected) { const Arc A = g.arcs[ac]; c = A.col; w = A.lat; }
+                                else { c = g.inCol[ac]; w = g.inLat[ac]; }
+                                const bool inF = ok && ((fbits[c >> 5] >> (c & 31)) & 1u);
+                                us[v][k] = inF ? c : -1;
+                                ws[v][k] = w;
+                            }
+#pragma unroll
+                        for (int v = 0; v < BV; ++v)
+#pragma unroll
+                            for (int k = 0; k < BK; ++k) {
+                                const int uu = us[v][k] >= 0 ? us[v][k] : (x[v] >= 0 ? x[v] : 0);
+                                du[v][k] = ld_wg(&D[(size_t)uu * LB + l]);
+                            }
+#pragma unroll
+                        for (int v = 0; v < BV; ++v)
+#pragma unroll
+                            for (int k = 0; k < BK; ++k) {
+                                if (us[v][k] < 0 || !(b2d(du[v][k]) < bound)) continue;
+                                const unsigned long long c = d2b(b2d(du[v][k]) + ws[v][k]);
+                                best[v] = c < best[v] ? c : best[v];
+                            }
+                        arcsDone += BK;
+                    }
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        const bool imp = x[v] >= 0 && best[v] < dxv[v];
+                        if (imp) __hip_atomic_store(&D[(size_t)x[v] * LB + l], best[v], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const uint32_t imask = (uint32_t)(__ballot(imp) >> gbase) & LBMASK;
+                        if (imask && l == 0) {
+                            atomicOr(&anyN[x[v] >> 5], 1u << (x[v] & 31));
+                            myAct = 1;
+                        }
+                    }
+                }
+            } else {
             // the queue entries of the group's NEXT vertices are loaded one
             // iteration ahead (qn >= 1 here), so a vertex starts with its
             // dist / row-range loads instead of a dependent queue round trip
@@ -349,6 +487,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                         }
                 }
             }
+            }   // push relax
             if (dbg && l == 0) {
                 const unsigned long long bz = (unsigned long long)((long long)clock64() - tg0);
                 atomicMax(&ctl->busyMax, bz);
@@ -769,9 +908,9 @@ static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch
                        bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, cfg.kflags);
 }
 
-int batch_lds_bytes(int n) {
+int batch_lds_bytes(int n, int kflags) {
     const int nwp = (((n + 31) >> 5) + 3) & ~3;
-    return 64 + 2 * 4 * nwp + 2 * 4 * (LMAX + 4);
+    return 64 + ((kflags & 4) ? 4 : 2) * 4 * nwp + 2 * 4 * (LMAX + 4);
 }
 
 const void* batch_kernel_ptr(int lb) {

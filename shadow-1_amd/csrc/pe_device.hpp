@@ -123,7 +123,7 @@ struct BatchLaunch {
     int32_t ldsBytes;
     double delta;            // bucket width
     int32_t kflags;          // variant bits: 1 plain stores in the relax phase (experiment),
-                             // 2 per-lane pending masks
+                             // 2 per-lane pending masks, 4 pull relax
 };
 
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)
@@ -163,7 +163,7 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, void* stream);
 const void* batch_kernel_ptr(int lb);
-int batch_lds_bytes(int n);
+int batch_lds_bytes(int n, int kflags);
 // dense path (pe_dense.hip)
 void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int64_t nArcs,
                         void* stream);

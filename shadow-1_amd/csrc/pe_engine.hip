@@ -264,7 +264,7 @@ static int configure(ShdPe* pe, Shard* sh) {
         b.lb = ((int64_t)sh->rowCount + 15) / 16 < (int64_t)sh->numCUs ? 8 : 16;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
-    b.ldsBytes = batch_lds_bytes((int)n);
+    b.ldsBytes = batch_lds_bytes((int)n, tu.batchKflags);
     if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
     int bPerCU = 1;
