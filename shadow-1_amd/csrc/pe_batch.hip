@@ -42,10 +42,13 @@ constexpr int BT_THREADS = 1024;
 constexpr int BK = 4;        // arcs per vertex per load batch
 constexpr int BV = 2;        // vertices interleaved per group
 constexpr int LMAX = 4096;   // depth levels bucketed in LDS (deeper -> sweeps)
+constexpr int ICH = 8;       // arcs per work item (kflags & 8)
 
 struct alignas(16) BCtrl {
     int qtail;
     int active;
+    int itail;
+    int pad2;
     unsigned long long minNext;
     unsigned int ambMask;
     int changed;
@@ -162,6 +165,11 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
     const bool masks = (kflags & 2) != 0;
     uint32_t* const PM0 = as_global(bs.pm + slot * 2 * NS);
     uint32_t* const PM1 = PM0 + NS;
+    // arc-chunk work items (kflags & 8): every active vertex becomes
+    // ceil(deg / ICH) items {u, a0, a1, active lanes}, so a hub's arcs are
+    // spread over all groups instead of one group setting the phase length
+    const bool split = (kflags & 8) != 0;
+    int4* const IT = reinterpret_cast<int4*>(as_global(bs.items)) + slot * (size_t)bs.itemCap;
 
     for (int b = blockIdx.x; b < nBatches; b += gridDim.x) {
         const int row = batchRows[(size_t)b * LB + l];
@@ -180,6 +188,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             if (tid == 0) {
                 ctl->qtail = 0;
                 ctl->active = 0;
+                ctl->itail = 0;
                 ctl->minNext = INF_BITS;
                 ctl->ambMask = 0u;
                 ctl->changed = 0;
@@ -382,6 +391,116 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                         }
                     }
                 }
+            } else if (split) {
+                // (B) candidates -> work items
+                for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
+                    int u[BV], a0[BV], a1[BV];
+                    uint32_t pmk[BV];
+                    unsigned long long db[BV];
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        const int uu = i0 + v < qn ? ld_wg(&Q[i0 + v]) : -1;
+                        const int uc = uu >= 0 ? uu : 0;
+                        const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                        const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
+                        pmk[v] = masks ? ld_wg(&PMc[uc]) : LBMASK;
+                        u[v] = uu;
+                        db[v] = uu >= 0 ? d0 : INF_BITS;
+                        a0[v] = uu >= 0 ? r0 : 0;
+                        a1[v] = uu >= 0 ? r1 : 0;
+                    }
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        if (u[v] < 0) continue;
+                        const bool pend = (pmk[v] >> l) & 1u;
+                        const bool act = pend && b2d(db[v]) < bound;
+                        const bool defer = pend && !act && db[v] != INF_BITS;
+                        const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
+                        const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
+                        if (masks && l == 0) {
+                            __hip_atomic_store(&PMc[u[v]], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (dmask) atomicOr(&PMn[u[v]], dmask);
+                        }
+                        if (l == 0 && dmask) atomicOr(&anyN[u[v] >> 5], 1u << (u[v] & 31));
+                        if (defer) myMin = db[v] < myMin ? db[v] : myMin;
+                        const int deg = a1[v] - a0[v];
+                        if (!amask || deg == 0) continue;
+                        ++procs;
+                        arcsDone += deg;
+                        lanesAct += __popc(amask);
+                        const int nIt = (deg + ICH - 1) / ICH;
+                        int base = 0;
+                        if (l == 0) base = atomicAdd(&ctl->itail, nIt);
+                        base = __shfl(base, gbase, 64);
+                        for (int k = l; k < nIt; k += LB)
+                            IT[base + k] = make_int4(u[v], a0[v] + k * ICH, min(a1[v], a0[v] + (k + 1) * ICH),
+                                                     (int)amask);
+                    }
+                }
+                fence_wg();
+                __syncthreads();
+                const int itn = ctl->itail;
+                // (C) items -> relaxations: every item is <= ICH arcs of one
+                // vertex; BV items per group, BK arcs per stage
+                for (int i0 = gid * BV; i0 < itn; i0 += NG * BV) {
+                    int u[BV], a0[BV], a1[BV];
+                    unsigned long long dub[BV];
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        const int4 it = i0 + v < itn ? IT[i0 + v] : make_int4(-1, 0, 0, 0);   // written before the barrier
+                        const int uc = it.x >= 0 ? it.x : 0;
+                        const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                        const bool act = it.x >= 0 && ((it.w >> l) & 1) && b2d(d0) < bound;
+                        u[v] = it.x;
+                        dub[v] = act ? d0 : INF_BITS;
+                        a0[v] = it.y;
+                        a1[v] = it.x >= 0 ? it.z : it.y;
+                    }
+                    int maxd = 0;
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) maxd = max(maxd, a1[v] - a0[v]);
+                    for (int t = 0; t < maxd; t += BK) {
+                        int xs[BV][BK];
+                        double ws[BV][BK];
+                        unsigned long long dx[BV][BK];
+#pragma unroll
+                        for (int v = 0; v < BV; ++v)
+#pragma unroll
+                            for (int k = 0; k < BK; ++k) {
+                                const int a = a0[v] + t + k;
+                                const bool ok = a < a1[v];
+                                const Arc A = g.arcs[ok ? a : 0];
+                                xs[v][k] = ok ? A.col : -1;
+                                ws[v][k] = A.lat;
+                            }
+#pragma unroll
+                        for (int v = 0; v < BV; ++v)
+#pragma unroll
+                            for (int k = 0; k < BK; ++k)
+                                dx[v][k] = ld_wg(&D[(size_t)(xs[v][k] >= 0 ? xs[v][k] : 0) * LB + l]);
+#pragma unroll
+                        for (int v = 0; v < BV; ++v)
+#pragma unroll
+                            for (int k = 0; k < BK; ++k) {
+                                const int x = xs[v][k];
+                                bool imp = false;
+                                if (x >= 0 && dub[v] != INF_BITS) {
+                                    const unsigned long long nb = d2b(b2d(dub[v]) + ws[v][k]);
+                                    if (nb < dx[v][k]) {
+                                        __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                                        imp = true;
+                                    }
+                                }
+                                const uint32_t imask = (uint32_t)(__ballot(imp) >> gbase) & LBMASK;
+                                if (imask && l == 0) {
+                                    atomicOr(&anyN[x >> 5], 1u << (x & 31));
+                                    if (masks) atomicOr(&PMn[x], imask);
+                                    myAct = 1;
+                                }
+                            }
+                    }
+                }
             } else {
             // the queue entries of the group's NEXT vertices are loaded one
             // iteration ahead (qn >= 1 here), so a vertex starts with its
@@ -509,6 +628,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             if (tid == 0) {
                 ctl->qtail = 0;
                 ctl->active = 0;
+                ctl->itail = 0;
                 ctl->minNext = INF_BITS;
                 if (dbg) {
                     dbg[16 * b + 12] += (int)(ctl->busyMax >> 10);

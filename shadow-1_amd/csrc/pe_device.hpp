@@ -112,6 +112,8 @@ struct BatchScratch {
     int32_t* P;              // [slot][nStride][LB] chosen IN-arc, -1 none
     int32_t* X;              // [slot][4][nStride*LB] pointer-jumping / level lists
     uint32_t* pm;            // [slot][2][nStride] pending lane masks (cur/next)
+    int32_t* items;          // [slot][itemCap] int4 arc-chunk work items
+    int64_t itemCap;         // items per slot (>= nArcs / 8 + n)
     int32_t* queue;          // [slot][nStride] phase candidate list
     int64_t nStride;         // >= n, multiple of 64
 };
@@ -123,7 +125,7 @@ struct BatchLaunch {
     int32_t ldsBytes;
     double delta;            // bucket width
     int32_t kflags;          // variant bits: 1 plain stores in the relax phase (experiment),
-                             // 2 per-lane pending masks, 4 pull relax
+                             // 2 per-lane pending masks, 4 pull relax, 8 arc-chunk items
 };
 
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)

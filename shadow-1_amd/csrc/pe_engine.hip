@@ -617,7 +617,8 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     if (sh->batchReady) return SHD_PE_OK;
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     const size_t LB = (size_t)sh->bcfg.lb;
-    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4 * 3;
+    const size_t itemCap = ((size_t)pe->hg.nArcs() + 7) / 8 + NS;
+    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4 * 3 + itemCap * 16;
     // scratch budget (default 64 GiB): fewer resident batches on huge graphs
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
@@ -625,11 +626,12 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     size_t slots = std::min<size_t>({(size_t)sh->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
     sh->bcfg.grid = (int32_t)slots;
     int rc;
-    void *D, *R, *H, *P, *X, *q, *pm, *rows, *amb;
+    void *D, *R, *H, *P, *X, *q, *pm, *it, *rows, *amb;
     if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &X, slots * NS * LB * 16)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
         (rc = dev_alloc(sh, &q, slots * NS * 4)) || (rc = dev_alloc(sh, &pm, slots * NS * 2 * 4)) ||
+        (rc = dev_alloc(sh, &it, slots * itemCap * 16)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
         (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)))
         return rc;
@@ -640,6 +642,8 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.X = (int32_t*)X;
     sh->bsc.queue = (int32_t*)q;
     sh->bsc.pm = (uint32_t*)pm;
+    sh->bsc.items = (int32_t*)it;
+    sh->bsc.itemCap = (int64_t)itemCap;
     sh->bsc.nStride = (int64_t)NS;
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
