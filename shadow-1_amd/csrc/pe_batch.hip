@@ -49,6 +49,7 @@ struct alignas(16) BCtrl {
     int active;
     int itail;
     int pad2;
+    unsigned long long maxDb;   // largest reached distance (bit pattern) of the batch
     unsigned long long minNext;
     unsigned int ambMask;
     int changed;
@@ -123,7 +124,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                                                            BatchScratch bs,
                                                            const int32_t* __restrict__ batchRows,
                                                            int32_t nBatches, uint8_t* rowAmbig,
-                                                           double delta, int32_t* dbg, int kflags) {
+                                                           double delta, int32_t* dbg, int kflags,
+                                                           double bw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                 ctl->qtail = 0;
                 ctl->active = 0;
                 ctl->itail = 0;
+                ctl->maxDb = 0ull;
                 ctl->minNext = INF_BITS;
                 ctl->ambMask = 0u;
                 ctl->changed = 0;
@@ -202,6 +205,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         if (gid == 0 && src >= 0) {
             D[(size_t)src * LB + l] = d2b(0.0);
             R[(size_t)src * LB + l] = 1.0;
+            H[(size_t)src * LB + l] = 0;
             atomicOr(&any0[src >> 5], 1u << (src & 31));
             if (masks) atomicOr(&PM0[src], 1u << l);
         }
@@ -655,6 +659,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         //     vertex (self for roots), depth 1 per tree arc.
         bool amb = false;
         int viol = 0;
+        unsigned long long myMaxD = 0ull;
         {
             uint32_t* const anyC = par ? any1 : any0;
             for (int v0 = gid * BV; v0 < n; v0 += NG * BV) {
@@ -748,6 +753,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                         atomicOr(&anyC[vv >> 5], 1u << (vv & 31));
                         if (masks) atomicOr(&(par ? PM1 : PM0)[vv], bm);
                     }
+                    if (dvb[v] != INF_BITS) myMaxD = dvb[v] > myMaxD ? dvb[v] : myMaxD;
                     const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
                     if (!root[v] && dvb[v] != INF_BITS && cnt[v] != 1) amb = true;
                     P[e] = tree ? ba[v] : -1;
@@ -757,6 +763,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         }
         if (amb) atomicOr(&ctl->ambMask, 1u << l);
         if (viol) ctl->changed = 1;
+        if (myMaxD) atomicMax(&ctl->maxDb, myMaxD);
         fence_wg();
         __syncthreads();
         const int anyViol = ctl->changed;
@@ -772,6 +779,40 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         }   // verification loop
         const long long tPh2 = dbg ? (long long)clock64() : 0;
 
+        // ================= 3+4. hops and reliability ========================
+        // Distance-bucket levels: with a bucket width bw below the smallest
+        // arc latency, every tree parent sits in a strictly earlier bucket
+        // of floor(dist / bw) (dist[v] = dist[parent] + w, w >= min latency
+        // > bw; the float sum and division are monotone to far below the
+        // 0.1% margin), so a counting sort of the entries by bucket is a
+        // topological order of every predecessor tree: one level loop gives
+        // hops[v] = hops[parent] + 1 and rel[v] = rel[parent] * r(parent, v)
+        // -- the reference's left fold (topology.c:1430, :1499) -- with one
+        // gather per entry and no pointer jumping.  Too many buckets (tiny
+        // latencies) -> pointer jumping + depth levels below.
+        const double maxD = b2d(ctl->maxDb);
+        const int nLev = bw > 0.0 && maxD / bw < (double)LMAX ? (int)(maxD / bw) + 1 : LMAX + 1;
+        int maxDepth = 0, rounds = 0;
+        int32_t* const Hc = H;
+        if (nLev <= LMAX) {
+            for (int k = tid; k <= nLev + 1; k += NT) hist[k] = 0;
+            __syncthreads();
+            for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
+                int kk[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const size_t e = e0 + (size_t)k * NT;
+                    const unsigned long long d = e < NE ? ld_wg(&D[e]) : INF_BITS;
+                    const int a = e < NE ? ld_wg(&P[e]) : -1;
+                    kk[k] = (a >= 0 && d != INF_BITS) ? (int)(b2d(d) / bw) : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wave_agg_add(hist, kk[k], kk[k] > 0);
+            }
+            maxDepth = nLev;     // the level count below
+            fence_wg();
+            __syncthreads();
+        } else {
         // ================= 3. hop counts: pointer jumping ====================
         // JH[e] = (J, H) packed in one 8-B word: H = tree distance from v to
         // its ancestor J; roots (and unreached entries) are (v, 0).  Jumping
@@ -780,7 +821,6 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         // values only jumps further.  Entries that already point at a root
         // are final and store ~H (negative): later rounds skip them without
         // touching their parent, and children jump straight to the root.
-        int rounds = 0;
         for (;;) {
             int ch = 0, dmax = 0;
             for (size_t e0 = (size_t)tid * 4; e0 < NE; e0 += (size_t)NT * 4) {
@@ -830,10 +870,9 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
             if (tid == 0) ctl->maxDepth = 0;
             __syncthreads();
         }
-        const int maxDepth = ctl->maxDepth;
+        maxDepth = ctl->maxDepth;
         // unpack the hop counts into H (0 for roots / unreached) and, for the
         // depth-ordered fold, histogram them
-        int32_t* const Hc = H;
         if (maxDepth <= LMAX) {
             for (int k = tid; k <= maxDepth + 1; k += NT) hist[k] = 0;
             __syncthreads();
@@ -855,6 +894,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         }
         fence_wg();
         __syncthreads();
+        }   // pointer jumping
+        const bool byDist = nLev <= LMAX;
         const long long tPh3 = dbg ? (long long)clock64() : 0;
 
         // ================= 4. reliability in depth order =====================
@@ -883,8 +924,14 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const size_t e = e0 + (size_t)k * NT;
-                    dd[k] = e < NE ? ld_wg(&Hc[e]) : 0;
-                    aa[k] = e < NE ? ld_wg(&P[e]) : 0;
+                    if (byDist) {
+                        const unsigned long long d = e < NE ? ld_wg(&D[e]) : INF_BITS;
+                        aa[k] = e < NE ? ld_wg(&P[e]) : -1;
+                        dd[k] = (aa[k] >= 0 && d != INF_BITS) ? (int)(b2d(d) / bw) : 0;
+                    } else {
+                        dd[k] = e < NE ? ld_wg(&Hc[e]) : 0;
+                        aa[k] = e < NE ? ld_wg(&P[e]) : 0;
+                    }
                 }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -913,14 +960,19 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                         xs[k] = g.inCol[a];
                         rr[k] = g.inRel[a];
                     }
+                    int hp[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         const int ll = (ea[k].x >= 0 ? ea[k].x : 0) % LB;
                         rp[k] = ld_wg(&R[(size_t)xs[k] * LB + ll]);
+                        hp[k] = byDist ? ld_wg(&Hc[(size_t)xs[k] * LB + ll]) : 0;
                     }
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
-                        if (ea[k].x >= 0) R[ea[k].x] = rp[k] * rr[k];
+                        if (ea[k].x >= 0) {
+                            R[ea[k].x] = rp[k] * rr[k];
+                            if (byDist) Hc[ea[k].x] = hp[k] + 1;
+                        }
                 }
                 fence_wg();
                 __syncthreads();
@@ -1025,7 +1077,7 @@ static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
     hipLaunchKernelGGL(k_batch_rows<LB>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
-                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, cfg.kflags);
+                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, cfg.kflags, cfg.bucketWidth);
 }
 
 int batch_lds_bytes(int n, int kflags) {

@@ -74,7 +74,8 @@ struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0, exactAos = 0;
-    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchKflags = 0, batchOrder = 0;
+    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchKflags = 0, batchOrder = 0,
+        batchBucketLevels = 1;
     double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
@@ -124,6 +125,7 @@ struct BatchLaunch {
     int32_t grid;            // resident workgroups (= scratch slots)
     int32_t ldsBytes;
     double delta;            // bucket width
+    double bucketWidth;      // distance-bucket level width (< min arc latency), 0 = off
     int32_t kflags;          // variant bits: 1 plain stores in the relax phase (experiment),
                              // 2 per-lane pending masks, 4 pull relax, 8 arc-chunk items
 };

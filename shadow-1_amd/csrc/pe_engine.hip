@@ -147,6 +147,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_GRID", t.batchGrid);
     gi("SHDPE_BATCH_KFLAGS", t.batchKflags);
     gi("SHDPE_BATCH_ORDER", t.batchOrder);
+    gi("SHDPE_BATCH_BUCKET_LEVELS", t.batchBucketLevels);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -280,6 +281,9 @@ static int configure(ShdPe* pe, Shard* sh) {
     b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
     if (!(b.delta > 0)) b.delta = 1.0;
     b.kflags = tu.batchKflags;
+    // hops / reliability by distance-bucket levels (pe_batch.hip): width just
+    // under the smallest arc latency; SHDPE_BATCH_BUCKET_LEVELS=0 disables
+    b.bucketWidth = tu.batchBucketLevels && g.minArcLatency > 0.0 ? g.minArcLatency * 0.999 : 0.0;
     sh->bcfg = b;
     sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
     sh->stats.batched = pe->batched ? 1 : 0;

@@ -232,14 +232,17 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     g->isComplete = complete;
     // mean arc latency (bucket width): fixed 64-chunk partial sums added in
     // order, so the value does not depend on the thread count
-    std::vector<double> part(64, 0.0);
+    std::vector<double> part(64, 0.0), pmin(64, INFINITY);
     par_chunks(nArcs, 64, nArcs, [&](int c, int64_t a0, int64_t a1) {
-        double s = 0.0;
-        for (int64_t a = a0; a < a1; ++a) s += g->lat[a];
+        double s = 0.0, mn = INFINITY;
+        for (int64_t a = a0; a < a1; ++a) { s += g->lat[a]; mn = std::min(mn, g->lat[a]); }
         part[c] = s;
+        pmin[c] = mn;
     });
-    double sum = 0.0;
+    double sum = 0.0, mn = INFINITY;
     for (double x : part) sum += x;
+    for (double x : pmin) mn = std::min(mn, x);
+    g->minArcLatency = nArcs ? mn : 0.0;
     g->meanArcLatency = nArcs ? sum / (double)nArcs : 1.0;
     return SHD_PE_OK;
 }

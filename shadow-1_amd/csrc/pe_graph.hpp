@@ -46,6 +46,7 @@ struct HostGraph {
     std::vector<uint8_t> hasSelf;
     bool isComplete = false;
     double meanArcLatency = 0.0;
+    double minArcLatency = 0.0;     // smallest non-loop arc latency (0: no arcs)
 
     int64_t nArcs() const { return (int64_t)col.size(); }
     // igraph_get_eid(from,to) restricted to simple graphs: arc index into the
