@@ -74,7 +74,7 @@ struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0, exactAos = 0;
-    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchKflags = 0, batchOrder = 0,
+    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 0,
         batchBucketLevels = 1;
     double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
@@ -102,32 +102,27 @@ struct DevScratch {
     int64_t stride;    // elements per slot (>= n)
 };
 
-// Batched multi-source kernel (pe_batch.hip): one slot per resident
-// workgroup; every per-vertex array is [n][LB] (LB sources of the batch
-// side by side, so one arc relaxation serves LB sources with one coalesced
-// access).
+// Batched multi-source kernels (pe_batch.hip): one slot per workgroup of a
+// round; every per-vertex array is [n][LB] (LB sources of the batch side by
+// side, so one arc relaxation serves LB sources with one coalesced access).
 struct BatchScratch {
     unsigned long long* D;   // [slot][nStride][LB] f64 bit patterns (dist)
     double* R;               // [slot][nStride][LB] rel product label
     int32_t* H;              // [slot][nStride][LB] hop label
     int32_t* P;              // [slot][nStride][LB] chosen IN-arc, -1 none
     int32_t* X;              // [slot][4][nStride*LB] pointer-jumping / level lists
-    uint32_t* pm;            // [slot][2][nStride] pending lane masks (cur/next)
-    int32_t* items;          // [slot][itemCap] int4 arc-chunk work items
-    int64_t itemCap;         // items per slot (>= nArcs / 8 + n)
     int32_t* queue;          // [slot][nStride] phase candidate list
+    void* info;              // [batch] per-batch relax results (pe_batch.hip BInfo)
     int64_t nStride;         // >= n, multiple of 64
 };
 
 struct BatchLaunch {
-    int32_t lb;              // sources per batch (8 or 16)
+    int32_t lb;              // sources per batch (8, 16 or 32)
     int32_t threads;         // workgroup size
-    int32_t grid;            // resident workgroups (= scratch slots)
-    int32_t ldsBytes;
+    int32_t grid;            // batches per round (= scratch slots)
+    int32_t ldsBytes;        // k_batch_relax dynamic LDS
     double delta;            // bucket width
     double bucketWidth;      // distance-bucket level width (< min arc latency), 0 = off
-    int32_t kflags;          // variant bits: 1 plain stores in the relax phase (experiment),
-                             // 2 per-lane pending masks, 4 pull relax, 8 arc-chunk items
 };
 
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)
@@ -167,7 +162,7 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, void* stream);
 const void* batch_kernel_ptr(int lb);
-int batch_lds_bytes(int n, int kflags);
+int batch_lds_bytes(int n);
 // dense path (pe_dense.hip)
 void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int64_t nArcs,
                         void* stream);

@@ -145,7 +145,6 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_LB", t.batchLB);
     gi("SHDPE_BATCH_THREADS", t.batchThreads);
     gi("SHDPE_BATCH_GRID", t.batchGrid);
-    gi("SHDPE_BATCH_KFLAGS", t.batchKflags);
     gi("SHDPE_BATCH_ORDER", t.batchOrder);
     gi("SHDPE_BATCH_BUCKET_LEVELS", t.batchBucketLevels);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
@@ -265,22 +264,12 @@ static int configure(ShdPe* pe, Shard* sh) {
         b.lb = ((int64_t)sh->rowCount + 15) / 16 < (int64_t)sh->numCUs ? 8 : 16;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
-    b.ldsBytes = batch_lds_bytes((int)n, tu.batchKflags);
+    b.ldsBytes = batch_lds_bytes((int)n);
     if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
-    int bPerCU = 1;
-    if (b.ldsBytes <= LDS &&
-        (hipFuncSetAttribute(batch_kernel_ptr(b.lb), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             b.ldsBytes) != hipSuccess ||
-         hipOccupancyMaxActiveBlocksPerMultiprocessor(&bPerCU, batch_kernel_ptr(b.lb), b.threads,
-                                                      b.ldsBytes) != hipSuccess ||
-         bPerCU < 1))
-        bPerCU = 1;
-    b.grid = sh->numCUs * bPerCU;
-    if (tu.batchGrid > 0 && tu.batchGrid < b.grid) b.grid = tu.batchGrid;
+    b.grid = 0;                       // batches per round: ensure_batch (memory budget)
     b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
     if (!(b.delta > 0)) b.delta = 1.0;
-    b.kflags = tu.batchKflags;
     // hops / reliability by distance-bucket levels (pe_batch.hip): width just
     // under the smallest arc latency; SHDPE_BATCH_BUCKET_LEVELS=0 disables
     b.bucketWidth = tu.batchBucketLevels && g.minArcLatency > 0.0 ? g.minArcLatency * 0.999 : 0.0;
@@ -621,21 +610,23 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     if (sh->batchReady) return SHD_PE_OK;
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     const size_t LB = (size_t)sh->bcfg.lb;
-    const size_t itemCap = ((size_t)pe->hg.nArcs() + 7) / 8 + NS;
-    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4 * 3 + itemCap * 16;
-    // scratch budget (default 64 GiB): fewer resident batches on huge graphs
+    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4;
+    // scratch budget (default 64 GiB) -> slots = batches per round; rounds
+    // of equal size (a short last round would leave CUs idle)
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
-    const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
-    const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
-    size_t slots = std::min<size_t>({(size_t)sh->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
+    size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
+    if (pe->tu.batchGrid > 0) maxSlots = std::min<size_t>(maxSlots, (size_t)pe->tu.batchGrid);
+    const size_t nBatchesAll = std::max<size_t>(1, ((size_t)sh->rowCount + LB - 1) / LB);
+    const size_t rounds = (nBatchesAll + maxSlots - 1) / maxSlots;
+    const size_t slots = (nBatchesAll + rounds - 1) / rounds;
     sh->bcfg.grid = (int32_t)slots;
     int rc;
-    void *D, *R, *H, *P, *X, *q, *pm, *it, *rows, *amb;
+    void *D, *R, *H, *P, *X, *q, *info, *rows, *amb;
     if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &X, slots * NS * LB * 16)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
-        (rc = dev_alloc(sh, &q, slots * NS * 4)) || (rc = dev_alloc(sh, &pm, slots * NS * 2 * 4)) ||
-        (rc = dev_alloc(sh, &it, slots * itemCap * 16)) ||
+        (rc = dev_alloc(sh, &q, slots * NS * 4)) ||
+        (rc = dev_alloc(sh, &info, (nBatchesAll + 64) * 16)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
         (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)))
         return rc;
@@ -645,9 +636,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.P = (int32_t*)P;
     sh->bsc.X = (int32_t*)X;
     sh->bsc.queue = (int32_t*)q;
-    sh->bsc.pm = (uint32_t*)pm;
-    sh->bsc.items = (int32_t*)it;
-    sh->bsc.itemCap = (int64_t)itemCap;
+    sh->bsc.info = info;
     sh->bsc.nStride = (int64_t)NS;
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
