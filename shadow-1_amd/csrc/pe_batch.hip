@@ -346,9 +346,9 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_relax(DevGraph g0, BatchSc
             ctl->active = 0;
             ctl->minNext = INF_BITS;
             if (dbg) {
-                dbg[16 * b + 12] += (int)(ctl->busyMax >> 10);
-                dbg[16 * b + 13] += (int)((ctl->busySum / NG) >> 10);
-                dbg[16 * b + 14] += qn;
+                dbg[32 * b + 12] += (int)(ctl->busyMax >> 10);
+                dbg[32 * b + 13] += (int)((ctl->busySum / NG) >> 10);
+                dbg[32 * b + 14] += qn;
                 ctl->busyMax = 0;
                 ctl->busySum = 0;
             }
@@ -360,13 +360,13 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_relax(DevGraph g0, BatchSc
     if (tid == 0) info[b] = BInfo{failed ? 1 : 0, phases, 0, 0};
     if (dbg) {
         if (tid == 0) {
-            dbg[16 * b + 0] = phases;
-            dbg[16 * b + 5] = (int)(((long long)clock64() - tPh0) >> 10);
+            dbg[32 * b + 0] = phases;
+            dbg[32 * b + 5] = (int)(((long long)clock64() - tPh0) >> 10);
         }
         if (l == 0 && procs) {
-            atomicAdd(&dbg[16 * b + 4], (int)procs);
-            atomicAdd(&dbg[16 * b + 9], (int)(arcsDone >> 4));
-            atomicAdd(&dbg[16 * b + 10], (int)lanesAct);
+            atomicAdd(&dbg[32 * b + 4], (int)procs);
+            atomicAdd(&dbg[32 * b + 9], (int)(arcsDone >> 4));
+            atomicAdd(&dbg[32 * b + 10], (int)lanesAct);
         }
     }
 }
@@ -406,7 +406,9 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable
     int32_t* P = as_global(bs.P + slot * SE);
     int32_t* const X = as_global(bs.X + slot * 4 * SE);
     unsigned long long* JH = reinterpret_cast<unsigned long long*>(X);   // 2 SE words
-    int2* LV = reinterpret_cast<int2*>(X + 2 * SE);                     // 2 SE words
+    // level lists (after the pointer jumping is done with JH): 16 B per tree
+    // entry {entry, parent entry, r(parent, v)}, all 4 SE words of X
+    int4* LV = reinterpret_cast<int4*>(X);
 
     const int row = batchRows[(size_t)b * LB + l];
     const int src = row >= 0 ? g.attached[row] : -1;
@@ -663,7 +665,9 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable
             if (tid == 0) { hist[nLev + 1] = carry; cur[nLev + 1] = carry; }
         }
         __syncthreads();
-        // counting-sort scatter: LV[pos] = (entry, its tree in-arc)
+        const long long tSc = dbg ? (long long)clock64() : 0;
+        // counting-sort scatter: LV[pos] = {entry, parent entry, arc rel};
+        // the arc lookups happen here, off the level loop's dependent chain
         for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
             int dd[4], aa[4];
 #pragma unroll
@@ -678,52 +682,97 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable
                     aa[k] = e < NE ? ld_wg(&P[e]) : 0;
                 }
             }
+            int px[4];
+            double pr[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int a = dd[k] > 0 ? aa[k] : 0;
+                px[k] = g.inCol[a];
+                pr[k] = g.inRel[a];
+            }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 int pos = -1;
                 if (byDist) { if (dd[k] > 0) pos = atomicAdd(&cur[dd[k]], 1); }
                 else pos = wave_agg_add(cur, dd[k], dd[k] > 0);
-                if (pos >= 0) LV[pos] = make_int2((int)(e0 + (size_t)k * NT), aa[k]);
+                if (pos >= 0) {
+                    const int e = (int)(e0 + (size_t)k * NT);
+                    const unsigned long long rb = (unsigned long long)__double_as_longlong(pr[k]);
+                    LV[pos] = make_int4(e, px[k] * LB + e % LB, (int)(uint32_t)rb, (int)(uint32_t)(rb >> 32));
+                }
             }
         }
         fence_wg();
         __syncthreads();
+        const long long tLv = dbg ? (long long)clock64() : 0;
         // level by level: rel[v] = rel[parent] * r(parent, v) (and, for
         // distance buckets, hops[v] = hops[parent] + 1); four entries per
         // thread in flight (a chain of dependent gathers)
+        // level by level: rel[v] = rel[parent] * r(parent, v) (and, for
+        // distance buckets, hops[v] = hops[parent] + 1).  The level's records
+        // were loaded before the previous barrier, so each level is one
+        // dependent gather (parent labels) and the stores.
+        long long lvWork = 0;
+        constexpr int LK = 4;                 // records per thread in flight
+        int4 nx[LK];
+        {
+            const int q0 = hist[1], q1 = hist[2];
+#pragma unroll
+            for (int k = 0; k < LK; ++k) {
+                const int q = q0 + tid + k * NT;
+                nx[k] = q < q1 ? LV[q] : make_int4(-1, 0, 0, 0);
+            }
+        }
         for (int d = 1; d <= nLev; ++d) {
             const int q0 = hist[d], q1 = hist[d + 1];
-            if (q0 == q1) continue;
-            for (int qb = q0 + tid; qb < q1; qb += NT * 4) {
-                int2 ea[4];
-                int xs[4], hp[4];
-                double rr[4], rp[4];
+            if (dbg && tid == 0) lvWork += q1 - q0;
+            int4 ea[LK];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int q = qb + k * NT;
-                    ea[k] = q < q1 ? LV[q] : make_int2(-1, 0);
+            for (int k = 0; k < LK; ++k) ea[k] = nx[k];
+            // records of the next level (independent of this level's results)
+            if (d < nLev) {
+                const int n0 = hist[d + 1], n1 = hist[d + 2];
+#pragma unroll
+                for (int k = 0; k < LK; ++k) {
+                    const int q = n0 + tid + k * NT;
+                    nx[k] = q < n1 ? LV[q] : make_int4(-1, 0, 0, 0);
+                }
+            }
+            for (int qb = q0 + tid;; qb += NT * LK) {
+                double rp[LK];
+                int hp[LK];
+#pragma unroll
+                for (int k = 0; k < LK; ++k) {
+                    const int pe = ea[k].x >= 0 ? ea[k].y : 0;
+                    rp[k] = ld_wg(&R[pe]);
+                    hp[k] = byDist ? ld_wg(&H[pe]) : 0;
                 }
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int a = ea[k].x >= 0 ? ea[k].y : 0;
-                    xs[k] = g.inCol[a];
-                    rr[k] = g.inRel[a];
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int ll = (ea[k].x >= 0 ? ea[k].x : 0) % LB;
-                    rp[k] = ld_wg(&R[(size_t)xs[k] * LB + ll]);
-                    hp[k] = byDist ? ld_wg(&H[(size_t)xs[k] * LB + ll]) : 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < LK; ++k)
                     if (ea[k].x >= 0) {
-                        R[ea[k].x] = rp[k] * rr[k];
+                        const double rr = __longlong_as_double(
+                            (long long)((unsigned long long)(uint32_t)ea[k].z |
+                                        ((unsigned long long)(uint32_t)ea[k].w << 32)));
+                        R[ea[k].x] = rp[k] * rr;
                         if (byDist) H[ea[k].x] = hp[k] + 1;
                     }
+                if (qb + NT * LK >= q1) break;
+                // more records than one pass of the workgroup (wide levels)
+#pragma unroll
+                for (int k = 0; k < LK; ++k) {
+                    const int q = qb + NT * LK + k * NT;
+                    ea[k] = q < q1 ? LV[q] : make_int4(-1, 0, 0, 0);
+                }
             }
             fence_wg();
             __syncthreads();
+        }
+        if (dbg && tid == 0) {
+            dbg[32 * b + 20] = (int)((tLv - tSc) >> 10);
+            dbg[32 * b + 16] = (int)lvWork;
+            dbg[32 * b + 17] = hist[nLev + 1];
+            dbg[32 * b + 18] = hist[1];
+            dbg[32 * b + 19] = nLev;
         }
     } else {
         // very deep trees: Gauss-Seidel sweeps until nothing changes
@@ -796,14 +845,14 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable
         }
     }
     if (dbg && tid == 0) {
-        dbg[16 * b + 1] = rounds;
-        dbg[16 * b + 2] = nLev - 1;
-        dbg[16 * b + 3] = (int)ambMask;
-        dbg[16 * b + 15] = ctl->viol;
-        dbg[16 * b + 6] = (int)((tPh2 - tPh1) >> 10);
-        dbg[16 * b + 7] = (int)((tPh3 - tPh2) >> 10);
-        dbg[16 * b + 11] = (int)((tPh4 - tPh3) >> 10);
-        dbg[16 * b + 8] = (int)(((long long)clock64() - tPh4) >> 10);
+        dbg[32 * b + 1] = rounds;
+        dbg[32 * b + 2] = nLev - 1;
+        dbg[32 * b + 3] = (int)ambMask;
+        dbg[32 * b + 15] = ctl->viol;
+        dbg[32 * b + 6] = (int)((tPh2 - tPh1) >> 10);
+        dbg[32 * b + 7] = (int)((tPh3 - tPh2) >> 10);
+        dbg[32 * b + 11] = (int)((tPh4 - tPh3) >> 10);
+        dbg[32 * b + 8] = (int)(((long long)clock64() - tPh4) >> 10);
     }
 }
 

@@ -684,7 +684,7 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
     long rnd = 0, dmax = 0, ambB = 0, rep = 0;
     double tMin = 1e30, tMax = 0, tSum = 0, tSq = 0;
     for (int32_t i = 0; i < nB; ++i) {
-        const int32_t* d = d0 + 16 * i;
+        const int32_t* d = d0 + 32 * i;
         ph += d[0]; rnd += d[1]; dmax = std::max<long>(dmax, d[2]);
         ambB += d[3] != 0;
         rep += d[15];
@@ -700,6 +700,12 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
     }
     const double mean = tSum / std::max(nB, 1);
     const double sd = std::sqrt(std::max(0.0, tSq / std::max(nB, 1) - mean * mean));
+    double lw = 0, ln = 0, lsc = 0;
+    for (int32_t i = 0; i < nB; ++i) {
+        lw += d0[32 * i + 16]; ln += d0[32 * i + 19]; lsc += 1024.0 * d0[32 * i + 20];
+    }
+    std::fprintf(stderr, "[shdpe] level loop entries/batch=%.0f levels=%.1f | scatter Mcycles/batch=%.2f (in rel)\n",
+                 lw / nB, ln / nB, lsc / nB / 1e6);
     std::fprintf(stderr, "[shdpe] shard %d batch relax Mcycles/batch: sum over phases of group-busy max=%.2f mean=%.2f | candidates/batch=%.0f\n",
                  sh->gindex, bmax / nB / 1e6, bmean / nB / 1e6, cand / nB);
     std::fprintf(stderr, "[shdpe] batch arc-visits/batch=%.0f (%.2f x nArcs) active lanes/proc=%.2f\n",
@@ -797,7 +803,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             order.resize((size_t)nB * LB, -1);
             HIPCHK(hipMemcpyAsync(sh->dBatchRows, order.data(), order.size() * 4,
                                   hipMemcpyHostToDevice, sh->stream));
-            if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 64, sh->stream));
+            if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 128, sh->stream));
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
                               sh->dDbg, sh->stream);
@@ -812,7 +818,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             for (size_t i = 0; i < order.size(); ++i)
                 if (order[i] >= 0 && amb[i]) exactRows.push_back(order[i]);
             if (sh->dDbg) {
-                std::vector<int32_t> dbg((size_t)nB * 16);
+                std::vector<int32_t> dbg((size_t)nB * 32);
                 HIPCHK(hipMemcpy(dbg.data(), sh->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
                 print_batch_debug(pe, sh, dbg.data(), nB);
             }
