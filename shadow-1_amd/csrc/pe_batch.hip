@@ -1,41 +1,36 @@
-// pe_batch.hip -- batched multi-source sparse kernels of the Shadow path
+// pe_batch.hip -- batched multi-source sparse kernel of the Shadow path
 // engine (gfx950).
 //
 // Reference semantics (Shadow v1.14.0, src/main/routing/topology.c): one
 // source row = _topology_computeSourcePaths (:1655-1875) = igraph 0.7.1
 // Dijkstra (:1765) + the per-target fold _topology_computePathProperties
-// (:1407-1523).  Same contract as k_sparse_rows (pe_kernels.hip); these
-// kernels are the layout for graphs whose per-row state does not fit LDS
-// (n of 10^5+).
+// (:1407-1523).  Same contract as k_sparse_rows (pe_kernels.hip); this kernel
+// is the layout for graphs whose per-row state does not fit LDS (n of 10^5+).
 //
-// A batch is LB sources.  Every per-vertex array is laid out [v][LB]: a
-// group of LB lanes handles one vertex for all LB sources (lane l = source
-// l), so one arc relaxation dist[u] + w -> dist[v] for LB sources is ONE
-// coalesced LB*8-byte access instead of LB random ones.  The per-source
-// distance rows (0.8-2 MB each) live in HBM.  Sources of a batch are chosen
-// close together in the graph (host-side order), so their frontiers
-// coincide.
+// One workgroup owns a batch of LB sources.  Every per-vertex array is laid
+// out [v][LB]: a group of LB lanes handles one vertex for all LB sources
+// (lane l = source l), so one arc relaxation dist[u] + w -> dist[v] for LB
+// sources is ONE coalesced LB*8-byte access instead of LB random ones.  The
+// per-source distance rows (0.8-2 MB each) live in HBM; loaded latency is
+// ~1.2 us per dependent access, so every stage keeps several independent
+// vertices per group in flight (V-way interleave) and the relaxation phase
+// carries no labels at all.  Sources of a batch are chosen close together in
+// the graph (host-side BFS rank), so their bucket frontiers coincide.
 //
-// Two kernels per round of batches (one workgroup per batch, one scratch
-// slot per workgroup; a round holds more batches than resident workgroups,
-// so the hardware balances batches of different cost across CUs):
-//   k_batch_relax  label-correcting delta-stepping with a shared bucket bound
-//                  and double-buffered per-vertex pending bits in LDS;
-//                  relaxations are dist[u] + w only (left fold -> igraph's
-//                  distances bit for bit), improvements
-//                  are no-return atomic mins (no lost update);
-//   k_batch_post   (a) Bellman check + predecessor: tight in-arc with minimum
-//                  dist[u] per lane = igraph's first-popped tight predecessor;
-//                  equal minima (or a zero-increment arc) make the row a tie
-//                  row for k_exact_rows; a violated Bellman inequality (never
-//                  with atomic relaxation) hands the whole batch to it too;
-//                  (b) hops and reliability in a topological order of the
-//                  predecessor trees -- distance buckets narrower than the
-//                  smallest arc latency, or (tiny latencies) tree depth from
-//                  pointer jumping -- one gather per entry:
-//                  hops = hops[parent] + 1, rel = rel[parent] * r, the
-//                  reference's left fold (topology.c:1430, :1499) exactly;
-//                  (c) the row writer (topology.c:1805-1864).
+// Per batch:
+//   1. label-correcting delta-stepping with a shared bucket bound and
+//      double-buffered per-vertex pending lane masks (cur/next); relaxations
+//      are dist[u] + w only (left fold -> igraph's distances bit for bit,
+//      SURVEY.md Appendix B);
+//   2. predecessor pass: tight in-arc with minimum dist[u] per lane = igraph's
+//      first-popped tight predecessor; equal minima (or a zero-increment arc)
+//      make the row a tie row for k_exact_rows;
+//   3. hop counts = depth in the predecessor forest, by pointer jumping
+//      (exact integer sums, log2(depth) rounds);
+//   4. reliability in depth order: entries bucketed by depth (counting sort
+//      in LDS), then level by level R[v] = R[parent] * rel(parent, v) -- the
+//      reference's left fold (topology.c:1430, :1499) exactly;
+//   5. the row writer (topology.c:1805-1864).
 #include <hip/hip_runtime.h>
 
 #include "pe_device.hpp"
@@ -46,31 +41,22 @@ namespace shdpe {
 constexpr int BT_THREADS = 1024;
 constexpr int BK = 4;        // arcs per vertex per load batch
 constexpr int BV = 2;        // vertices interleaved per group
-constexpr int LMAX = 4096;   // levels bucketed in LDS (more -> pointer jumping / sweeps)
+constexpr int LMAX = 4096;   // depth levels bucketed in LDS (deeper -> sweeps)
 
-// per-batch results handed from k_batch_relax to k_batch_post
-struct alignas(16) BInfo {
-    int failed;              // phase cap hit: rows go to k_exact_rows
-    int phases;
-    int pad0, pad1;
-};
-
-struct alignas(16) RCtrl {
+struct alignas(16) BCtrl {
     int qtail;
     int active;
     unsigned long long minNext;
+    unsigned int ambMask;
+    int changed;
+    int maxDepth;
+    int pad;
     unsigned long long busyMax;
     unsigned long long busySum;
 };
 
-struct alignas(16) PCtrl {
-    unsigned long long maxDb;   // largest reached distance (bit pattern)
-    unsigned int ambMask;
-    int viol;
-    int changed;
-    int maxDepth;
-};
-
+// Forward reliability fold with vertex factors (topology.c:1430-1462, :1499)
+// along lane l's predecessor chain, multiplied in source -> target order.
 // packed pointer-jumping entry: low word = ancestor J, high word = H
 __device__ __forceinline__ int jh_j(unsigned long long w) { return (int)(uint32_t)w; }
 __device__ __forceinline__ int jh_h(unsigned long long w) { return (int)(uint32_t)(w >> 32); }
@@ -80,7 +66,7 @@ __device__ __forceinline__ void st_jh(unsigned long long* p, int j, int h) {
 }
 
 // Wave-aggregated counter add: the lanes of a wave that bump the same
-// counter (tree depths: ~20 distinct keys for 10^6 entries) are merged into
+// counter (depth levels: ~20 distinct keys for 10^6 entries) are merged into
 // one LDS atomic per distinct key instead of serialising 64 same-address
 // atomics.  Returns each participating lane's slot (old value + its rank).
 __device__ __forceinline__ int wave_agg_add(int* ctr, int key, bool act) {
@@ -105,7 +91,7 @@ __device__ __forceinline__ int wave_agg_add(int* ctr, int key, bool act) {
 // Forward reliability fold with vertex factors (topology.c:1430-1462, :1499)
 // along lane l's predecessor chain, multiplied in source -> target order:
 // the chain is walked in blocks of 64 factors from the source end (O(h)
-// loads per block, O(h^2 / 64) in all; no per-thread scratch).
+// loads per block, O(h^2 / 64) in all; no per-thread scratch beyond 64).
 template <int LB>
 __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
                                               const double* __restrict__ inRel,
@@ -130,24 +116,15 @@ __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
     return acc;
 }
 
-// ===========================================================================
-// k_batch_relax: label-correcting delta-stepping over one batch.
-// ===========================================================================
-// Pending state is one bit per VERTEX (LDS): "some lane of u improved".  A
-// candidate processes every lane with dist < bound: re-relaxing a lane that
-// did not change costs no memory traffic (the group reads the whole
-// dist[x][0..LB) line anyway) and never improves anything.  Lanes at or above
-// the bound keep the vertex pending (deferred); the bound only grows, so such
-// a lane has never been processed at its current value.  Improvements are
-// no-return atomic mins at workgroup scope: the line was just read for the
-// pre-check, so the atomic resolves in L2, and no update is lost.
 template <int LB>
-__global__ __launch_bounds__(BT_THREADS) void k_batch_relax(DevGraph g0, BatchScratch bs,
-                                                            const int32_t* __restrict__ batchRows,
-                                                            int32_t b0, double delta, BInfo* info,
-                                                            int32_t* dbg) {
+__global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable tab0,
+                                                           BatchScratch bs,
+                                                           const int32_t* __restrict__ batchRows,
+                                                           int32_t nBatches, uint8_t* rowAmbig,
+                                                           double delta, int32_t* dbg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const DevGraph g = global_view(g0);
+    const DevTable tab = global_view(tab0);
     constexpr unsigned int LBMASK = LB >= 32 ? 0xFFFFFFFFu : ((1u << (LB & 31)) - 1u);
     const int n = g.n;
     const int nw = (n + 31) >> 5;
@@ -156,248 +133,16 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_relax(DevGraph g0, BatchSc
     const int l = tid % LB;
     const int gid = tid / LB, NG = NT / LB;
     const int gbase = (tid & 63) - l;       // first lane of my group in the wave
-    const size_t NE = (size_t)n * LB;
+    const bool undirected = g.inCol == g.col;
+    const size_t NE = (size_t)n * LB;        // (vertex, lane) entries
 
-    RCtrl* ctl = reinterpret_cast<RCtrl*>(smem);
+    BCtrl* ctl = reinterpret_cast<BCtrl*>(smem);
     uint32_t* const any0 = reinterpret_cast<uint32_t*>(smem + 64);
     uint32_t* const any1 = any0 + nwp;
+    int32_t* const hist = reinterpret_cast<int32_t*>(any1 + nwp);   // [LMAX + 2]
+    int32_t* const cur = hist + (LMAX + 4);                           // [LMAX + 2]
 
     const size_t slot = blockIdx.x;
-    const int b = b0 + (int)slot;
-    const size_t NS = (size_t)bs.nStride;
-    const size_t SE = NS * LB;
-    unsigned long long* D = as_global(bs.D + slot * SE);
-    double* R = as_global(bs.R + slot * SE);
-    int32_t* H = as_global(bs.H + slot * SE);
-    int32_t* Q = as_global(bs.queue + slot * NS);
-
-    const int row = batchRows[(size_t)b * LB + l];
-    const int src = row >= 0 ? g.attached[row] : -1;
-    // ---- init: dist = +inf for all (v, lane); pending sets empty ----
-    {
-        ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
-        const size_t cnt2 = NE / 2;
-        const ulonglong2 inf2 = make_ulonglong2(INF_BITS, INF_BITS);
-        for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
-        for (int w = tid; w < nwp; w += NT) { any0[w] = 0u; any1[w] = 0u; }
-        if (tid == 0) {
-            ctl->qtail = 0;
-            ctl->active = 0;
-            ctl->minNext = INF_BITS;
-            ctl->busyMax = 0;
-            ctl->busySum = 0;
-        }
-    }
-    fence_wg();
-    __syncthreads();
-    if (gid == 0 && src >= 0) {
-        D[(size_t)src * LB + l] = d2b(0.0);
-        R[(size_t)src * LB + l] = 1.0;
-        H[(size_t)src * LB + l] = 0;
-        atomicOr(&any0[src >> 5], 1u << (src & 31));
-    }
-    fence_wg();
-    __syncthreads();
-
-    int par = 0, phases = 0;
-    bool failed = false;
-    const int phaseCap = 8 * n + 1024;
-    long long procs = 0, arcsDone = 0, lanesAct = 0;
-    double bound = delta;
-    const long long tPh0 = dbg ? (long long)clock64() : 0;
-    for (;;) {
-        uint32_t* const anyC = par ? any1 : any0;
-        uint32_t* const anyN = par ? any0 : any1;
-        // candidates = vertices with a pending bit (cur set, consumed)
-        for (int w = tid; w < nw; w += NT) {
-            uint32_t bits = anyC[w];
-            if (bits) {
-                anyC[w] = 0u;
-                int pos = atomicAdd(&ctl->qtail, __popc(bits));
-                while (bits) {
-                    const int bb = __ffs(bits) - 1;
-                    bits &= bits - 1;
-                    Q[pos++] = (w << 5) + bb;
-                }
-            }
-        }
-        fence_wg();
-        __syncthreads();
-        const int qn = ctl->qtail;
-        if (qn == 0) break;
-        if (phases > phaseCap) {        // safety net: never spin the GPU
-            failed = true;
-            break;
-        }
-        unsigned long long myMin = INF_BITS;
-        int myAct = 0;
-        const long long tg0 = dbg ? (long long)clock64() : 0;
-        // the queue entries of the group's NEXT vertices are loaded one
-        // iteration ahead (qn >= 1 here), so a vertex starts with its dist /
-        // row-range loads instead of a dependent queue round trip
-        int nq[BV];
-#pragma unroll
-        for (int v = 0; v < BV; ++v) {
-            const int idx = gid * BV + v;
-            nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
-        }
-        for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
-            int u[BV], a0[BV], a1[BV];
-            unsigned long long db[BV], dub[BV];
-#pragma unroll
-            for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? nq[v] : -1;
-#pragma unroll
-            for (int v = 0; v < BV; ++v) {
-                const int idx = i0 + NG * BV + v;
-                nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
-            }
-#pragma unroll
-            for (int v = 0; v < BV; ++v) {
-                // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
-                const int uc = u[v] >= 0 ? u[v] : 0;
-                const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
-                const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
-                db[v] = u[v] >= 0 ? d0 : INF_BITS;
-                a0[v] = u[v] >= 0 ? r0 : 0;
-                a1[v] = u[v] >= 0 ? r1 : 0;
-            }
-            int maxd = 0;
-#pragma unroll
-            for (int v = 0; v < BV; ++v) {
-                const bool act = b2d(db[v]) < bound;
-                const bool defer = !act && db[v] != INF_BITS;
-                const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
-                const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                if (l == 0 && dmask) atomicOr(&anyN[u[v] >> 5], 1u << (u[v] & 31));
-                if (defer) myMin = db[v] < myMin ? db[v] : myMin;
-                dub[v] = act ? db[v] : INF_BITS;
-                if (!amask) a1[v] = a0[v];
-                else if (dbg) {
-                    ++procs;
-                    arcsDone += a1[v] - a0[v];
-                    lanesAct += __popc(amask);
-                }
-                maxd = max(maxd, a1[v] - a0[v]);
-            }
-            // relax u's out-arcs for the lanes below the bound
-            for (int t = 0; t < maxd; t += BK) {
-                int xs[BV][BK];
-                double ws[BV][BK];
-                unsigned long long dx[BV][BK];
-                // branch-free: out-of-range slots load arc 0 / vertex 0 and
-                // are masked, so all BV*BK loads of a stage are in flight
-                // before the first wait
-#pragma unroll
-                for (int v = 0; v < BV; ++v)
-#pragma unroll
-                    for (int k = 0; k < BK; ++k) {
-                        const int a = a0[v] + t + k;
-                        const bool ok = a < a1[v];
-                        const Arc A = g.arcs[ok ? a : 0];
-                        xs[v][k] = ok ? A.col : -1;
-                        ws[v][k] = A.lat;
-                    }
-#pragma unroll
-                for (int v = 0; v < BV; ++v)
-#pragma unroll
-                    for (int k = 0; k < BK; ++k)
-                        dx[v][k] = ld_wg(&D[(size_t)(xs[v][k] >= 0 ? xs[v][k] : 0) * LB + l]);
-#pragma unroll
-                for (int v = 0; v < BV; ++v)
-#pragma unroll
-                    for (int k = 0; k < BK; ++k) {
-                        const int x = xs[v][k];
-                        bool imp = false;
-                        if (x >= 0) {
-                            const unsigned long long nb = d2b(b2d(dub[v]) + ws[v][k]);
-                            if (nb < dx[v][k]) {
-                                __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                                imp = true;
-                            }
-                        }
-                        if (__ballot(imp) >> gbase & LBMASK && l == 0) {
-                            atomicOr(&anyN[x >> 5], 1u << (x & 31));
-                            myAct = 1;
-                        }
-                    }
-            }
-        }
-        if (dbg && l == 0) {
-            const unsigned long long bz = (unsigned long long)((long long)clock64() - tg0);
-            atomicMax(&ctl->busyMax, bz);
-            atomicAdd(&ctl->busySum, bz);
-        }
-        if (myMin != INF_BITS) atomicMin(&ctl->minNext, myMin);
-        if (myAct) ctl->active = 1;
-        fence_wg();
-        __syncthreads();
-        if (!ctl->active) {
-            // no relaxation improved anything: the bucket is settled, jump to
-            // the bucket of the smallest deferred distance
-            const double mn = b2d(ctl->minNext);
-            double nb = (floor(mn / delta) + 1.0) * delta;
-            if (!(mn < nb)) nb = mn + delta;
-            bound = nb;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            ctl->qtail = 0;
-            ctl->active = 0;
-            ctl->minNext = INF_BITS;
-            if (dbg) {
-                dbg[32 * b + 12] += (int)(ctl->busyMax >> 10);
-                dbg[32 * b + 13] += (int)((ctl->busySum / NG) >> 10);
-                dbg[32 * b + 14] += qn;
-                ctl->busyMax = 0;
-                ctl->busySum = 0;
-            }
-        }
-        par ^= 1;
-        ++phases;
-        __syncthreads();
-    }
-    if (tid == 0) info[b] = BInfo{failed ? 1 : 0, phases, 0, 0};
-    if (dbg) {
-        if (tid == 0) {
-            dbg[32 * b + 0] = phases;
-            dbg[32 * b + 5] = (int)(((long long)clock64() - tPh0) >> 10);
-        }
-        if (l == 0 && procs) {
-            atomicAdd(&dbg[32 * b + 4], (int)procs);
-            atomicAdd(&dbg[32 * b + 9], (int)(arcsDone >> 4));
-            atomicAdd(&dbg[32 * b + 10], (int)lanesAct);
-        }
-    }
-}
-
-// ===========================================================================
-// k_batch_post: predecessors, hops, reliability and the row writer.
-// ===========================================================================
-template <int LB>
-__global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable tab0,
-                                                           BatchScratch bs,
-                                                           const int32_t* __restrict__ batchRows,
-                                                           int32_t b0, uint8_t* rowAmbig,
-                                                           const BInfo* info, double bw,
-                                                           int32_t* dbg) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const DevGraph g = global_view(g0);
-    const DevTable tab = global_view(tab0);
-    constexpr unsigned int LBMASK = LB >= 32 ? 0xFFFFFFFFu : ((1u << (LB & 31)) - 1u);
-    const int n = g.n;
-    const int tid = threadIdx.x, NT = blockDim.x;
-    const int l = tid % LB;
-    const int gid = tid / LB, NG = NT / LB;
-    const bool undirected = g.inCol == g.col;
-    const size_t NE = (size_t)n * LB;
-
-    PCtrl* ctl = reinterpret_cast<PCtrl*>(smem);
-    int32_t* const hist = reinterpret_cast<int32_t*>(smem + 64);     // [LMAX + 4]
-    int32_t* const cur = hist + (LMAX + 4);                           // [LMAX + 4]
-
-    const size_t slot = blockIdx.x;
-    const int b = b0 + (int)slot;
     const size_t NS = (size_t)bs.nStride;
     const size_t SE = NS * LB;
     unsigned long long* D = as_global(bs.D + slot * SE);
@@ -406,171 +151,351 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable
     int32_t* P = as_global(bs.P + slot * SE);
     int32_t* const X = as_global(bs.X + slot * 4 * SE);
     unsigned long long* JH = reinterpret_cast<unsigned long long*>(X);   // 2 SE words
-    // level lists (after the pointer jumping is done with JH): 16 B per tree
-    // entry {entry, parent entry, r(parent, v)}, all 4 SE words of X
-    int4* LV = reinterpret_cast<int4*>(X);
+    int2* LV = reinterpret_cast<int2*>(X + 2 * SE);                     // 2 SE words
+    int32_t* Q = as_global(bs.queue + slot * NS);
 
-    const int row = batchRows[(size_t)b * LB + l];
-    const int src = row >= 0 ? g.attached[row] : -1;
-    if (tid == 0) {
-        ctl->maxDb = 0ull;
-        ctl->ambMask = 0u;
-        ctl->viol = 0;
-        ctl->changed = 0;
-        ctl->maxDepth = 0;
-    }
-    __syncthreads();
-    const long long tPh1 = dbg ? (long long)clock64() : 0;
-
-    // ---- (a) Bellman check + predecessor pass ----
-    // every entry must satisfy dist[v] <= dist[u] + w for all in-arcs; igraph
-    // sets parent[v] from the first POPPED tight predecessor: the tight in-arc
-    // with minimum dist[u]; equal minima from distinct vertices (or a
-    // zero-increment arc) -> the heap decides -> tie row (k_exact_rows).
-    // Also seeds the pointer jumping: J = parent vertex (self for roots).
-    const bool needJH = !(bw > 0.0);    // bucket levels may still fall back below
-    bool amb = false;
-    int viol = 0;
-    unsigned long long myMaxD = 0ull;
-    for (int v0 = gid * BV; v0 < n; v0 += NG * BV) {
-        int a0[BV], a1[BV], ba[BV], cnt[BV], bu[BV];
-        unsigned long long dvb[BV], best[BV], mn[BV];
-        bool root[BV];
-#pragma unroll
-        for (int v = 0; v < BV; ++v) {
-            const int vv = v0 + v;
-            if (vv < n) {
-                dvb[v] = ld_wg(&D[(size_t)vv * LB + l]);
-                a0[v] = undirected ? g.rowPtr[vv] : g.inPtr[vv];
-                a1[v] = undirected ? g.rowPtr[vv + 1] : g.inPtr[vv + 1];
-            } else {
-                dvb[v] = INF_BITS;
-                a0[v] = a1[v] = 0;
+    for (int b = blockIdx.x; b < nBatches; b += gridDim.x) {
+        const int row = batchRows[(size_t)b * LB + l];
+        const int src = row >= 0 ? g.attached[row] : -1;
+        // ---- init: dist = +inf for all (v, lane); pending sets empty ----
+        {
+            ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
+            const size_t cnt2 = NE / 2;
+            const ulonglong2 inf2 = make_ulonglong2(INF_BITS, INF_BITS);
+            for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
+            for (int w = tid; w < nwp; w += NT) { any0[w] = 0u; any1[w] = 0u; }
+            if (tid == 0) {
+                ctl->qtail = 0;
+                ctl->active = 0;
+                ctl->minNext = INF_BITS;
+                ctl->ambMask = 0u;
+                ctl->changed = 0;
+                ctl->maxDepth = 0;
+                ctl->busyMax = 0;
+                ctl->busySum = 0;
             }
-            root[v] = vv == src || src < 0;
-            best[v] = INF_BITS;
-            mn[v] = INF_BITS;
-            cnt[v] = 0;
-            ba[v] = -1;
-            bu[v] = -1;
-        }
-        int maxd = 0;
-#pragma unroll
-        for (int v = 0; v < BV; ++v) maxd = max(maxd, a1[v] - a0[v]);
-        for (int t = 0; t < maxd; t += BK) {
-            int cu[BV][BK];
-            double lw[BV][BK];
-            unsigned long long du[BV][BK];
-#pragma unroll
-            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                for (int k = 0; k < BK; ++k) {      // branch-free (see the relax loop)
-                    const int a = a0[v] + t + k;
-                    const bool ok = a < a1[v];
-                    const int ac = ok ? a : 0;
-                    int c;
-                    if (undirected) {
-                        const Arc A = g.arcs[ac];
-                        c = A.col;
-                        lw[v][k] = A.lat;
-                    } else {
-                        c = g.inCol[ac];
-                        lw[v][k] = g.inLat[ac];
-                    }
-                    cu[v][k] = ok ? c : -1;
-                }
-#pragma unroll
-            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                for (int k = 0; k < BK; ++k) {
-                    const unsigned long long t2 = ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]);
-                    du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
-                }
-#pragma unroll
-            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                for (int k = 0; k < BK; ++k) {
-                    if (cu[v][k] < 0 || root[v]) continue;
-                    const double cand = b2d(du[v][k]) + lw[v][k];
-                    const unsigned long long cb = d2b(cand);
-                    mn[v] = cb < mn[v] ? cb : mn[v];
-                    if (dvb[v] != INF_BITS && du[v][k] <= dvb[v] && cand == b2d(dvb[v])) {
-                        if (du[v][k] == dvb[v]) amb = true;   // zero-increment arc
-                        if (du[v][k] < best[v]) {
-                            best[v] = du[v][k];
-                            cnt[v] = 1;
-                            ba[v] = a0[v] + t + k;
-                            bu[v] = cu[v][k];
-                        } else if (du[v][k] == best[v]) {
-                            ++cnt[v];
-                        }
-                    }
-                }
-        }
-#pragma unroll
-        for (int v = 0; v < BV; ++v) {
-            const int vv = v0 + v;
-            if (vv >= n) continue;
-            const size_t e = (size_t)vv * LB + l;
-            if (!root[v] && mn[v] < dvb[v]) viol = 1;
-            if (dvb[v] != INF_BITS) myMaxD = dvb[v] > myMaxD ? dvb[v] : myMaxD;
-            const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
-            if (!root[v] && dvb[v] != INF_BITS && cnt[v] != 1) amb = true;
-            P[e] = tree ? ba[v] : -1;
-            if (needJH) st_jh(&JH[e], tree ? bu[v] : vv, tree ? 1 : 0);
-        }
-    }
-    if (amb) atomicOr(&ctl->ambMask, 1u << l);
-    if (viol) ctl->viol = 1;
-    if (myMaxD) atomicMax(&ctl->maxDb, myMaxD);
-    fence_wg();
-    __syncthreads();
-    uint32_t ambMask = ctl->ambMask;
-    // a violated Bellman inequality (a lost update: never with atomic
-    // relaxation) or the phase cap: the exact kernel recomputes the rows
-    if (ctl->viol || info[b].failed) ambMask = LBMASK;
-    const long long tPh2 = dbg ? (long long)clock64() : 0;
-
-    // ---- (b) hops and reliability ----
-    // Distance-bucket levels: with a bucket width bw below the smallest arc
-    // latency, every tree parent sits in a strictly earlier bucket of
-    // floor(dist / bw) (dist[v] = dist[parent] + w with w >= min latency >
-    // bw; the float sum and division are monotone far below the 0.1%
-    // margin), so a counting sort of the entries by bucket is a topological
-    // order of every predecessor tree.  Too many buckets (tiny latencies) ->
-    // tree depth by pointer jumping instead.
-    const double maxD = b2d(ctl->maxDb);
-    const bool byDist = bw > 0.0 && maxD / bw < (double)LMAX;
-    int nLev = 0, rounds = 0;
-    if (!byDist && !needJH) {
-        // bucket levels were planned but the batch is too deep for them:
-        // seed the pointer jumping now
-        for (size_t e = tid; e < NE; e += NT) {
-            const int a = ld_wg(&P[e]);
-            const int v = (int)(e / LB);
-            st_jh(&JH[e], a >= 0 ? g.inCol[a] : v, a >= 0 ? 1 : 0);
         }
         fence_wg();
         __syncthreads();
-    }
-    if (byDist) {
-        nLev = (int)(maxD / bw) + 1;
-        for (int k = tid; k <= nLev + 1; k += NT) hist[k] = 0;
-        __syncthreads();
-        // keys are spread over many buckets: plain LDS atomics
-        for (size_t e = tid; e < NE; e += NT) {
-            const unsigned long long d = ld_wg(&D[e]);
-            const int a = ld_wg(&P[e]);
-            if (a >= 0 && d != INF_BITS) atomicAdd(&hist[(int)(b2d(d) / bw)], 1);
+        if (gid == 0 && src >= 0) {
+            D[(size_t)src * LB + l] = d2b(0.0);
+            R[(size_t)src * LB + l] = 1.0;
+            atomicOr(&any0[src >> 5], 1u << (src & 31));
         }
-    } else {
-        // ---- tree depth by pointer jumping ----
+        fence_wg();
+        __syncthreads();
+
+        // ================= 1. delta-stepping over the batch =================
+        // Pending state is one bit per VERTEX (LDS): "some lane of u improved".
+        // A candidate processes every lane with dist < bound: re-relaxing a
+        // lane that did not change costs no memory traffic (the group reads
+        // the whole dist[x][0..LB) line anyway) and never improves anything.
+        // Lanes at or above the bound keep the vertex pending (deferred);
+        // the bound only grows, so such a lane has never been processed at
+        // its current value.  Improvements are no-return atomic mins at
+        // workgroup scope: the line was just read for the pre-check, so the
+        // atomic resolves in L2, and no update is lost.  (Plain stores lost
+        // ~1 update per batch to concurrent groups, and the Bellman repair
+        // that caught it -- a second relax + predecessor pass -- cost 20% of
+        // the relax phase at C4.)  The Bellman check of pass 2 stays as the
+        // safety net.
+        const long long tPh0 = dbg ? (long long)clock64() : 0;
+        long long tPh1 = 0;
+        int par = 0, phases = 0, repairs = 0;
+        bool failed = false;
+        const int phaseCap = 8 * n + 1024;
+        long long procs = 0, arcsDone = 0, lanesAct = 0;
+        double bound = delta;
+        uint32_t ambMask = 0u;
+        for (;;) {   // phases + verification until the Bellman check holds
+        for (;;) {
+            uint32_t* const anyC = par ? any1 : any0;
+            uint32_t* const anyN = par ? any0 : any1;
+            // candidates = vertices with a pending bit (cur set, consumed)
+            for (int w = tid; w < nw; w += NT) {
+                uint32_t bits = anyC[w];
+                if (bits) {
+                    anyC[w] = 0u;
+                    int pos = atomicAdd(&ctl->qtail, __popc(bits));
+                    while (bits) {
+                        const int bb = __ffs(bits) - 1;
+                        bits &= bits - 1;
+                        Q[pos++] = (w << 5) + bb;
+                    }
+                }
+            }
+            fence_wg();
+            __syncthreads();
+            const int qn = ctl->qtail;
+            if (qn == 0) break;
+            if (phases > phaseCap) {        // safety net: never spin the GPU
+                failed = true;
+                break;
+            }
+            unsigned long long myMin = INF_BITS;
+            int myAct = 0;
+            const long long tg0 = dbg ? (long long)clock64() : 0;
+            // the queue entries of the group's NEXT vertices are loaded one
+            // iteration ahead (qn >= 1 here), so a vertex starts with its
+            // dist / row-range loads instead of a dependent queue round trip
+            int nq[BV];
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                const int idx = gid * BV + v;
+                nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
+            }
+            for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
+                int u[BV], a0[BV], a1[BV];
+                unsigned long long db[BV], dub[BV];
+#pragma unroll
+                for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? nq[v] : -1;
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    const int idx = i0 + NG * BV + v;
+                    nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
+                }
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
+                    const int uc = u[v] >= 0 ? u[v] : 0;
+                    const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                    const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
+                    db[v] = u[v] >= 0 ? d0 : INF_BITS;
+                    a0[v] = u[v] >= 0 ? r0 : 0;
+                    a1[v] = u[v] >= 0 ? r1 : 0;
+                }
+                int maxd = 0;
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    const bool act = b2d(db[v]) < bound;
+                    const bool defer = !act && db[v] != INF_BITS;
+                    const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
+                    const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
+                    if (l == 0 && dmask) atomicOr(&anyN[u[v] >> 5], 1u << (u[v] & 31));
+                    if (defer) myMin = db[v] < myMin ? db[v] : myMin;
+                    dub[v] = act ? db[v] : INF_BITS;
+                    if (!amask) a1[v] = a0[v];
+                    else {
+                        ++procs;
+                        arcsDone += a1[v] - a0[v];
+                        lanesAct += __popc(amask);
+                    }
+                    maxd = max(maxd, a1[v] - a0[v]);
+                }
+                // relax u's out-arcs for the lanes below the bound
+                for (int t = 0; t < maxd; t += BK) {
+                    int xs[BV][BK];
+                    double ws[BV][BK];
+                    unsigned long long dx[BV][BK];
+                    // branch-free: out-of-range slots load arc 0 / vertex 0
+                    // and are masked, so all BV*BK loads of a stage are in
+                    // flight before the first wait
+#pragma unroll
+                    for (int v = 0; v < BV; ++v)
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            const int a = a0[v] + t + k;
+                            const bool ok = a < a1[v];
+                            const Arc A = g.arcs[ok ? a : 0];
+                            xs[v][k] = ok ? A.col : -1;
+                            ws[v][k] = A.lat;
+                        }
+#pragma unroll
+                    for (int v = 0; v < BV; ++v)
+#pragma unroll
+                        for (int k = 0; k < BK; ++k)
+                            dx[v][k] = ld_wg(&D[(size_t)(xs[v][k] >= 0 ? xs[v][k] : 0) * LB + l]);
+#pragma unroll
+                    for (int v = 0; v < BV; ++v)
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            const int x = xs[v][k];
+                            bool imp = false;
+                            if (x >= 0) {
+                                const unsigned long long nb = d2b(b2d(dub[v]) + ws[v][k]);
+                                if (nb < dx[v][k]) {
+                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    imp = true;
+                                }
+                            }
+                            if (__ballot(imp) >> gbase & LBMASK && l == 0) {
+                                atomicOr(&anyN[x >> 5], 1u << (x & 31));
+                                myAct = 1;
+                            }
+                        }
+                }
+            }
+            if (dbg && l == 0) {
+                const unsigned long long bz = (unsigned long long)((long long)clock64() - tg0);
+                atomicMax(&ctl->busyMax, bz);
+                atomicAdd(&ctl->busySum, bz);
+            }
+            if (myMin != INF_BITS) atomicMin(&ctl->minNext, myMin);
+            if (myAct) ctl->active = 1;
+            fence_wg();
+            __syncthreads();
+            if (!ctl->active) {
+                // no relaxation improved anything: the bucket is settled, jump
+                // to the bucket of the smallest deferred distance
+                const double mn = b2d(ctl->minNext);
+                double nb = (floor(mn / delta) + 1.0) * delta;
+                if (!(mn < nb)) nb = mn + delta;
+                bound = nb;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                ctl->qtail = 0;
+                ctl->active = 0;
+                ctl->minNext = INF_BITS;
+                if (dbg) {
+                    dbg[16 * b + 12] += (int)(ctl->busyMax >> 10);
+                    dbg[16 * b + 13] += (int)((ctl->busySum / NG) >> 10);
+                    dbg[16 * b + 14] += qn;
+                    ctl->busyMax = 0;
+                    ctl->busySum = 0;
+                }
+            }
+            par ^= 1;
+            ++phases;
+            __syncthreads();
+        }
+        if (dbg) tPh1 = (long long)clock64();
+
+        // ================= 2. Bellman check + predecessor pass ===============
+        // (a) every entry must satisfy dist[v] <= dist[u] + w for all in-arcs
+        //     (a violation = an update lost to a concurrent plain store: fix
+        //     it, mark v pending, and go back to phase 1);
+        // (b) igraph sets parent[v] from the first POPPED tight predecessor:
+        //     the tight in-arc with minimum dist[u]; equal minima from distinct
+        //     vertices (or a zero-increment arc) -> the heap decides -> tie
+        //     row (k_exact_rows).  Also seeds the pointer jumping: J = parent
+        //     vertex (self for roots), depth 1 per tree arc.
+        bool amb = false;
+        int viol = 0;
+        {
+            uint32_t* const anyC = par ? any1 : any0;
+            for (int v0 = gid * BV; v0 < n; v0 += NG * BV) {
+                int a0[BV], a1[BV], ba[BV], cnt[BV], bu[BV];
+                unsigned long long dvb[BV], best[BV], mn[BV];
+                bool root[BV];
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    const int vv = v0 + v;
+                    if (vv < n) {
+                        dvb[v] = ld_wg(&D[(size_t)vv * LB + l]);
+                        a0[v] = undirected ? g.rowPtr[vv] : g.inPtr[vv];
+                        a1[v] = undirected ? g.rowPtr[vv + 1] : g.inPtr[vv + 1];
+                    } else {
+                        dvb[v] = INF_BITS;
+                        a0[v] = a1[v] = 0;
+                    }
+                    root[v] = vv == src || src < 0;
+                    best[v] = INF_BITS;
+                    mn[v] = INF_BITS;
+                    cnt[v] = 0;
+                    ba[v] = -1;
+                    bu[v] = -1;
+                }
+                int maxd = 0;
+#pragma unroll
+                for (int v = 0; v < BV; ++v) maxd = max(maxd, a1[v] - a0[v]);
+                for (int t = 0; t < maxd; t += BK) {
+                    int cu[BV][BK];
+                    double lw[BV][BK];
+                    unsigned long long du[BV][BK];
+#pragma unroll
+                    for (int v = 0; v < BV; ++v)
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {      // branch-free (see pass 1)
+                            const int a = a0[v] + t + k;
+                            const bool ok = a < a1[v];
+                            const int ac = ok ? a : 0;
+                            int c;
+                            if (undirected) {
+                                const Arc A = g.arcs[ac];
+                                c = A.col;
+                                lw[v][k] = A.lat;
+                            } else {
+                                c = g.inCol[ac];
+                                lw[v][k] = g.inLat[ac];
+                            }
+                            cu[v][k] = ok ? c : -1;
+                        }
+#pragma unroll
+                    for (int v = 0; v < BV; ++v)
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            const unsigned long long t2 =
+                                ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]);
+                            du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
+                        }
+#pragma unroll
+                    for (int v = 0; v < BV; ++v)
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            if (cu[v][k] < 0 || root[v]) continue;
+                            const double cand = b2d(du[v][k]) + lw[v][k];
+                            const unsigned long long cb = d2b(cand);
+                            mn[v] = cb < mn[v] ? cb : mn[v];
+                            if (dvb[v] != INF_BITS && du[v][k] <= dvb[v] && cand == b2d(dvb[v])) {
+                                if (du[v][k] == dvb[v]) amb = true;   // zero-increment arc
+                                if (du[v][k] < best[v]) {
+                                    best[v] = du[v][k];
+                                    cnt[v] = 1;
+                                    ba[v] = a0[v] + t + k;
+                                    bu[v] = cu[v][k];
+                                } else if (du[v][k] == best[v]) {
+                                    ++cnt[v];
+                                }
+                            }
+                        }
+                }
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    const int vv = v0 + v;
+                    if (vv >= n) continue;
+                    const size_t e = (size_t)vv * LB + l;
+                    const bool bad = !root[v] && mn[v] < dvb[v];
+                    if (bad) {
+                        D[e] = mn[v];
+                        viol = 1;
+                    }
+                    const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
+                    if (bm && l == 0) atomicOr(&anyC[vv >> 5], 1u << (vv & 31));
+                    const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
+                    if (!root[v] && dvb[v] != INF_BITS && cnt[v] != 1) amb = true;
+                    P[e] = tree ? ba[v] : -1;
+                    st_jh(&JH[e], tree ? bu[v] : vv, tree ? 1 : 0);
+                }
+            }
+        }
+        if (amb) atomicOr(&ctl->ambMask, 1u << l);
+        if (viol) ctl->changed = 1;
+        fence_wg();
+        __syncthreads();
+        const int anyViol = ctl->changed;
+        ambMask = ctl->ambMask;
+        __syncthreads();
+        if (tid == 0) {
+            ctl->changed = 0;
+            ctl->ambMask = 0u;
+        }
+        __syncthreads();
+        if (!anyViol || failed) break;
+        ++repairs;
+        }   // verification loop
+        const long long tPh2 = dbg ? (long long)clock64() : 0;
+
+        // ================= 3. hop counts: pointer jumping ====================
         // JH[e] = (J, H) packed in one 8-B word: H = tree distance from v to
         // its ancestor J; roots (and unreached entries) are (v, 0).  Jumping
         // is in place: every read sees SOME consistent pair (single 8-B
         // accesses), each a valid (ancestor, distance), so mixing old and new
         // values only jumps further.  Entries that already point at a root
-        // are final and store ~H (negative): later rounds skip them.
+        // are final and store ~H (negative): later rounds skip them without
+        // touching their parent, and children jump straight to the root.
+        int rounds = 0;
         for (;;) {
             int ch = 0, dmax = 0;
             for (size_t e0 = (size_t)tid * 4; e0 < NE; e0 += (size_t)NT * 4) {
@@ -620,11 +545,12 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable
             if (tid == 0) ctl->maxDepth = 0;
             __syncthreads();
         }
-        nLev = ctl->maxDepth + 1;
-        // unpack the hop counts into H (0 for roots / unreached) and, for
-        // the depth-ordered fold, histogram them
-        if (nLev <= LMAX) {
-            for (int k = tid; k <= nLev + 1; k += NT) hist[k] = 0;
+        const int maxDepth = ctl->maxDepth;
+        // unpack the hop counts into H (0 for roots / unreached) and, for the
+        // depth-ordered fold, histogram them
+        int32_t* const Hc = H;
+        if (maxDepth <= LMAX) {
+            for (int k = tid; k <= maxDepth + 1; k += NT) hist[k] = 0;
             __syncthreads();
         }
         for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
@@ -638,268 +564,208 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_post(DevGraph g0, DevTable
             for (int k = 0; k < 4; ++k) {
                 const size_t e = e0 + (size_t)k * NT;
                 const int d = hh[k] < 0 ? ~hh[k] : 0;
-                if (e < NE) H[e] = d;
-                if (nLev <= LMAX) wave_agg_add(hist, d, e < NE && d > 0);
-            }
-        }
-    }
-    fence_wg();
-    __syncthreads();
-    const long long tPh3 = dbg ? (long long)clock64() : 0;
-    if (nLev <= LMAX) {
-        if (tid < 64) {
-            // exclusive scan of hist[1..nLev] by one wave
-            int carry = 0;
-            for (int base = 1; base <= nLev; base += 64) {
-                const int k = base + tid;
-                const int x = k <= nLev ? hist[k] : 0;
-                int s = x;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int y = __shfl_up(s, o, 64);
-                    if (tid >= o) s += y;
-                }
-                if (k <= nLev) { hist[k] = carry + s - x; cur[k] = carry + s - x; }
-                carry += __shfl(s, 63, 64);
-            }
-            if (tid == 0) { hist[nLev + 1] = carry; cur[nLev + 1] = carry; }
-        }
-        __syncthreads();
-        const long long tSc = dbg ? (long long)clock64() : 0;
-        // counting-sort scatter: LV[pos] = {entry, parent entry, arc rel};
-        // the arc lookups happen here, off the level loop's dependent chain
-        for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
-            int dd[4], aa[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const size_t e = e0 + (size_t)k * NT;
-                if (byDist) {
-                    const unsigned long long d = e < NE ? ld_wg(&D[e]) : INF_BITS;
-                    aa[k] = e < NE ? ld_wg(&P[e]) : -1;
-                    dd[k] = (aa[k] >= 0 && d != INF_BITS) ? (int)(b2d(d) / bw) : 0;
-                } else {
-                    dd[k] = e < NE ? ld_wg(&H[e]) : 0;
-                    aa[k] = e < NE ? ld_wg(&P[e]) : 0;
-                }
-            }
-            int px[4];
-            double pr[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int a = dd[k] > 0 ? aa[k] : 0;
-                px[k] = g.inCol[a];
-                pr[k] = g.inRel[a];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                int pos = -1;
-                if (byDist) { if (dd[k] > 0) pos = atomicAdd(&cur[dd[k]], 1); }
-                else pos = wave_agg_add(cur, dd[k], dd[k] > 0);
-                if (pos >= 0) {
-                    const int e = (int)(e0 + (size_t)k * NT);
-                    const unsigned long long rb = (unsigned long long)__double_as_longlong(pr[k]);
-                    LV[pos] = make_int4(e, px[k] * LB + e % LB, (int)(uint32_t)rb, (int)(uint32_t)(rb >> 32));
-                }
+                if (e < NE) Hc[e] = d;
+                if (maxDepth <= LMAX) wave_agg_add(hist, d, e < NE && d > 0);
             }
         }
         fence_wg();
         __syncthreads();
-        const long long tLv = dbg ? (long long)clock64() : 0;
-        // level by level: rel[v] = rel[parent] * r(parent, v) (and, for
-        // distance buckets, hops[v] = hops[parent] + 1); four entries per
-        // thread in flight (a chain of dependent gathers)
-        // level by level: rel[v] = rel[parent] * r(parent, v) (and, for
-        // distance buckets, hops[v] = hops[parent] + 1).  The level's records
-        // were loaded before the previous barrier, so each level is one
-        // dependent gather (parent labels) and the stores.
-        long long lvWork = 0;
-        constexpr int LK = 4;                 // records per thread in flight
-        int4 nx[LK];
-        {
-            const int q0 = hist[1], q1 = hist[2];
+        const long long tPh3 = dbg ? (long long)clock64() : 0;
+
+        // ================= 4. reliability in depth order =====================
+        if (maxDepth <= LMAX) {
+            if (tid < 64) {
+                // exclusive scan of hist[1..maxDepth] by one wave
+                int carry = 0;
+                for (int base = 1; base <= maxDepth; base += 64) {
+                    const int k = base + tid;
+                    const int x = k <= maxDepth ? hist[k] : 0;
+                    int s = x;
 #pragma unroll
-            for (int k = 0; k < LK; ++k) {
-                const int q = q0 + tid + k * NT;
-                nx[k] = q < q1 ? LV[q] : make_int4(-1, 0, 0, 0);
-            }
-        }
-        for (int d = 1; d <= nLev; ++d) {
-            const int q0 = hist[d], q1 = hist[d + 1];
-            if (dbg && tid == 0) lvWork += q1 - q0;
-            int4 ea[LK];
-#pragma unroll
-            for (int k = 0; k < LK; ++k) ea[k] = nx[k];
-            // records of the next level (independent of this level's results)
-            if (d < nLev) {
-                const int n0 = hist[d + 1], n1 = hist[d + 2];
-#pragma unroll
-                for (int k = 0; k < LK; ++k) {
-                    const int q = n0 + tid + k * NT;
-                    nx[k] = q < n1 ? LV[q] : make_int4(-1, 0, 0, 0);
-                }
-            }
-            for (int qb = q0 + tid;; qb += NT * LK) {
-                double rp[LK];
-                int hp[LK];
-#pragma unroll
-                for (int k = 0; k < LK; ++k) {
-                    const int pe = ea[k].x >= 0 ? ea[k].y : 0;
-                    rp[k] = ld_wg(&R[pe]);
-                    hp[k] = byDist ? ld_wg(&H[pe]) : 0;
-                }
-#pragma unroll
-                for (int k = 0; k < LK; ++k)
-                    if (ea[k].x >= 0) {
-                        const double rr = __longlong_as_double(
-                            (long long)((unsigned long long)(uint32_t)ea[k].z |
-                                        ((unsigned long long)(uint32_t)ea[k].w << 32)));
-                        R[ea[k].x] = rp[k] * rr;
-                        if (byDist) H[ea[k].x] = hp[k] + 1;
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int y = __shfl_up(s, o, 64);
+                        if (tid >= o) s += y;
                     }
-                if (qb + NT * LK >= q1) break;
-                // more records than one pass of the workgroup (wide levels)
+                    if (k <= maxDepth) { hist[k] = carry + s - x; cur[k] = carry + s - x; }
+                    carry += __shfl(s, 63, 64);
+                }
+                if (tid == 0) { hist[maxDepth + 1] = carry; cur[maxDepth + 1] = carry; }
+            }
+            __syncthreads();
+            // counting-sort scatter: LV[pos] = (entry, its tree in-arc)
+            for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
+                int dd[4], aa[4];
 #pragma unroll
-                for (int k = 0; k < LK; ++k) {
-                    const int q = qb + NT * LK + k * NT;
-                    ea[k] = q < q1 ? LV[q] : make_int4(-1, 0, 0, 0);
+                for (int k = 0; k < 4; ++k) {
+                    const size_t e = e0 + (size_t)k * NT;
+                    dd[k] = e < NE ? ld_wg(&Hc[e]) : 0;
+                    aa[k] = e < NE ? ld_wg(&P[e]) : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int pos = wave_agg_add(cur, dd[k], dd[k] > 0);
+                    if (pos >= 0) LV[pos] = make_int2((int)(e0 + (size_t)k * NT), aa[k]);
                 }
             }
             fence_wg();
             __syncthreads();
+            // level by level; four entries per thread in flight (the level
+            // loop is a chain of dependent gathers, latency-bound otherwise)
+            for (int d = 1; d <= maxDepth; ++d) {
+                const int q0 = hist[d], q1 = hist[d + 1];
+                for (int qb = q0 + tid; qb < q1; qb += NT * 4) {
+                    int2 ea[4];
+                    int xs[4];
+                    double rr[4], rp[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int q = qb + k * NT;
+                        ea[k] = q < q1 ? LV[q] : make_int2(-1, 0);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int a = ea[k].x >= 0 ? ea[k].y : 0;
+                        xs[k] = g.inCol[a];
+                        rr[k] = g.inRel[a];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int ll = (ea[k].x >= 0 ? ea[k].x : 0) % LB;
+                        rp[k] = ld_wg(&R[(size_t)xs[k] * LB + ll]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (ea[k].x >= 0) R[ea[k].x] = rp[k] * rr[k];
+                }
+                fence_wg();
+                __syncthreads();
+            }
+        } else {
+            // very deep trees: Gauss-Seidel sweeps until nothing changes
+            for (;;) {
+                if (tid == 0) ctl->changed = 0;
+                __syncthreads();
+                int ch = 0;
+                for (size_t e = tid; e < NE; e += NT) {
+                    const int a = ld_wg(&P[e]);
+                    const int v = (int)(e / LB), ll = (int)(e % LB);
+                    if (a < 0 || v == src) continue;
+                    const int x = g.inCol[a];
+                    const double er = ld_wg(&R[(size_t)x * LB + ll]) * g.inRel[a];
+                    if (ld_wg(&R[e]) != er) { R[e] = er; ch = 1; }
+                }
+                if (ch) ctl->changed = 1;
+                fence_wg();
+                __syncthreads();
+                if (!ctl->changed) break;
+                __syncthreads();
+            }
         }
+        const long long tPh4 = dbg ? (long long)clock64() : 0;
+        if (failed) ambMask = LBMASK;     // hand every row to k_exact_rows
+        if (gid == 0 && row >= 0) rowAmbig[(size_t)b * LB + l] = (ambMask >> l) & 1u;
         if (dbg && tid == 0) {
-            dbg[32 * b + 20] = (int)((tLv - tSc) >> 10);
-            dbg[32 * b + 16] = (int)lvWork;
-            dbg[32 * b + 17] = hist[nLev + 1];
-            dbg[32 * b + 18] = hist[1];
-            dbg[32 * b + 19] = nLev;
+            dbg[16 * b + 0] = phases;
+            dbg[16 * b + 1] = rounds;
+            dbg[16 * b + 2] = maxDepth;
+            dbg[16 * b + 3] = (int)ambMask;
+            dbg[16 * b + 15] = repairs;
+            dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
+            dbg[16 * b + 6] = (int)((tPh2 - tPh1) >> 10);
+            dbg[16 * b + 7] = (int)((tPh3 - tPh2) >> 10);
+            dbg[16 * b + 11] = (int)((tPh4 - tPh3) >> 10);
         }
-    } else {
-        // very deep trees: Gauss-Seidel sweeps until nothing changes
-        for (;;) {
-            if (tid == 0) ctl->changed = 0;
-            __syncthreads();
-            int ch = 0;
-            for (size_t e = tid; e < NE; e += NT) {
-                const int a = ld_wg(&P[e]);
-                const int v = (int)(e / LB), ll = (int)(e % LB);
-                if (a < 0 || v == src) continue;
-                const int x = g.inCol[a];
-                const double er = ld_wg(&R[(size_t)x * LB + ll]) * g.inRel[a];
-                if (ld_wg(&R[e]) != er) { R[e] = er; ch = 1; }
-            }
-            if (ch) ctl->changed = 1;
-            fence_wg();
-            __syncthreads();
-            if (!ctl->changed) break;
-            __syncthreads();
+        if (dbg && l == 0 && procs) {
+            atomicAdd(&dbg[16 * b + 4], (int)procs);
+            atomicAdd(&dbg[16 * b + 9], (int)(arcsDone >> 4));
+            atomicAdd(&dbg[16 * b + 10], (int)lanesAct);
         }
-    }
-    const long long tPh4 = dbg ? (long long)clock64() : 0;
-    if (gid == 0 && row >= 0) rowAmbig[(size_t)b * LB + l] = (ambMask >> l) & 1u;
 
-    // ---- (c) row writer (topology.c:1805-1864) ----
-    if (row >= 0 && !((ambMask >> l) & 1u)) {
-        const int T = (int)tab.T;
-        const size_t base = (size_t)(row - tab.rowStart) * (size_t)tab.T;
-        for (int j = gid; j < T; j += NG) {
-            const int t = g.attached[j];
-            double L = 0.0, Rl = 0.0;
-            int h = -1, pv = -1;
-            uint8_t f = 0;
-            if (t == src) {
-                // 1-vertex igraph path [s]: the fold uses edge (s,s)
-                // (:1469-1488); the destination factor is skipped (:1457)
-                if (g.hasSelf[src]) {
-                    L = 0.0 + g.selfLat[src];
-                    Rl = (1.0 * g.vrel[src]) * g.selfRel[src];
-                    h = 1;
+        // ================= 5. row writer (topology.c:1805-1864) ==============
+        if (row >= 0 && !((ambMask >> l) & 1u)) {
+            const int T = (int)tab.T;
+            const size_t base = (size_t)(row - tab.rowStart) * (size_t)tab.T;
+            for (int j = gid; j < T; j += NG) {
+                const int t = g.attached[j];
+                double L = 0.0, Rl = 0.0;
+                int h = -1, pv = -1;
+                uint8_t f = 0;
+                if (t == src) {
+                    // 1-vertex igraph path [s]: the fold uses edge (s,s)
+                    // (:1469-1488); the destination factor is skipped (:1457)
+                    if (g.hasSelf[src]) {
+                        L = 0.0 + g.selfLat[src];
+                        Rl = (1.0 * g.vrel[src]) * g.selfRel[src];
+                        h = 1;
+                    } else {
+                        f |= F_NOEDGE;
+                    }
                 } else {
-                    f |= F_NOEDGE;
-                }
-            } else {
-                const size_t e = (size_t)t * LB + l;
-                const unsigned long long dt = ld_wg(&D[e]);
-                if (dt == INF_BITS) {
-                    f |= F_UNREACHABLE;
-                } else {
-                    L = b2d(dt);
-                    h = ld_wg(&H[e]);
-                    const int pa = ld_wg(&P[e]);
-                    pv = pa >= 0 ? g.inCol[pa] : -1;
-                    if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
-                        Rl = ld_wg(&R[e]);
-                    else
-                        Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
-                    if (L == 0.0) {                 // topology.c:1848-1852
-                        L = 1.0;
-                        f |= F_ZEROLAT;
+                    const size_t e = (size_t)t * LB + l;
+                    const unsigned long long dt = ld_wg(&D[e]);
+                    if (dt == INF_BITS) {
+                        f |= F_UNREACHABLE;
+                    } else {
+                        L = b2d(dt);
+                        h = ld_wg(&Hc[e]);
+                        const int pa = ld_wg(&P[e]);
+                        pv = pa >= 0 ? g.inCol[pa] : -1;
+                        if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
+                            Rl = ld_wg(&R[e]);
+                        else
+                            Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
+                        if (L == 0.0) {                 // topology.c:1848-1852
+                            L = 1.0;
+                            f |= F_ZEROLAT;
+                        }
                     }
                 }
+                tab.lat[base + j] = L;
+                tab.rel[base + j] = Rl;
+                tab.hops[base + j] = h;
+                tab.flags[base + j] = f;
+                if (tab.pred) tab.pred[base + j] = pv;
             }
-            tab.lat[base + j] = L;
-            tab.rel[base + j] = Rl;
-            tab.hops[base + j] = h;
-            tab.flags[base + j] = f;
-            if (tab.pred) tab.pred[base + j] = pv;
         }
+        fence_wg();
+        __syncthreads();
+        if (dbg && tid == 0) dbg[16 * b + 8] = (int)(((long long)clock64() - tPh4) >> 10);
     }
-    if (dbg && tid == 0) {
-        dbg[32 * b + 1] = rounds;
-        dbg[32 * b + 2] = nLev - 1;
-        dbg[32 * b + 3] = (int)ambMask;
-        dbg[32 * b + 15] = ctl->viol;
-        dbg[32 * b + 6] = (int)((tPh2 - tPh1) >> 10);
-        dbg[32 * b + 7] = (int)((tPh3 - tPh2) >> 10);
-        dbg[32 * b + 11] = (int)((tPh4 - tPh3) >> 10);
-        dbg[32 * b + 8] = (int)(((long long)clock64() - tPh4) >> 10);
-    }
-}
-
-// ---------------------------------------------------------------------------
-int batch_lds_bytes(int n) {
-    const int nwp = (((n + 31) >> 5) + 3) & ~3;
-    return 64 + 2 * 4 * nwp;
-}
-
-static int post_lds_bytes() { return 64 + 2 * 4 * (LMAX + 4); }
-
-const void* batch_kernel_ptr(int lb) {
-    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_relax<8>);
-    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_relax<32>);
-    return reinterpret_cast<const void*>(&k_batch_relax<16>);
 }
 
 template <int LB>
 static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
-                      const BatchLaunch& cfg, int32_t* dDbg, hipStream_t st) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_relax<LB>),
+                      const BatchLaunch& cfg, int32_t* dDbg, hipStream_t st, int grid) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_post<LB>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, post_lds_bytes());
-    BInfo* info = reinterpret_cast<BInfo*>(bs.info);
-    // rounds of `grid` batches (= scratch slots): relax all, then post all
-    for (int b0 = 0; b0 < nBatches; b0 += cfg.grid) {
-        const int nb = nBatches - b0 < cfg.grid ? nBatches - b0 : cfg.grid;
-        hipLaunchKernelGGL(k_batch_relax<LB>, dim3(nb), dim3(cfg.threads), cfg.ldsBytes, st, g, bs,
-                           dBatchRows, b0, cfg.delta, info, dDbg);
-        hipLaunchKernelGGL(k_batch_post<LB>, dim3(nb), dim3(cfg.threads), post_lds_bytes(), st, g,
-                           tab, bs, dBatchRows, b0, dRowAmbig, info, cfg.bucketWidth, dDbg);
-    }
+    hipLaunchKernelGGL(k_batch_rows<LB>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
+                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg);
+}
+
+int batch_lds_bytes(int n) {
+    const int nwp = (((n + 31) >> 5) + 3) & ~3;
+    return 64 + 2 * 4 * nwp + 2 * 4 * (LMAX + 4);
+}
+
+const void* batch_kernel_ptr(int lb) {
+    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8>);
+    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32>);
+    return reinterpret_cast<const void*>(&k_batch_rows<16>);
 }
 
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, void* stream) {
     if (nBatches <= 0) return;
+    const int grid = nBatches < cfg.grid ? nBatches : cfg.grid;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (cfg.lb == 8)
-        launch_lb<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st);
+        launch_lb<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st, grid);
     else if (cfg.lb == 32)
-        launch_lb<32>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st);
+        launch_lb<32>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st, grid);
     else
-        launch_lb<16>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st);
+        launch_lb<16>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st, grid);
 }
 
 }  // namespace shdpe

@@ -74,8 +74,7 @@ struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0, exactAos = 0;
-    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 0,
-        batchBucketLevels = 1;
+    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 0;
     double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
@@ -102,9 +101,10 @@ struct DevScratch {
     int64_t stride;    // elements per slot (>= n)
 };
 
-// Batched multi-source kernels (pe_batch.hip): one slot per workgroup of a
-// round; every per-vertex array is [n][LB] (LB sources of the batch side by
-// side, so one arc relaxation serves LB sources with one coalesced access).
+// Batched multi-source kernel (pe_batch.hip): one slot per resident
+// workgroup; every per-vertex array is [n][LB] (LB sources of the batch
+// side by side, so one arc relaxation serves LB sources with one coalesced
+// access).
 struct BatchScratch {
     unsigned long long* D;   // [slot][nStride][LB] f64 bit patterns (dist)
     double* R;               // [slot][nStride][LB] rel product label
@@ -112,17 +112,15 @@ struct BatchScratch {
     int32_t* P;              // [slot][nStride][LB] chosen IN-arc, -1 none
     int32_t* X;              // [slot][4][nStride*LB] pointer-jumping / level lists
     int32_t* queue;          // [slot][nStride] phase candidate list
-    void* info;              // [batch] per-batch relax results (pe_batch.hip BInfo)
     int64_t nStride;         // >= n, multiple of 64
 };
 
 struct BatchLaunch {
     int32_t lb;              // sources per batch (8, 16 or 32)
     int32_t threads;         // workgroup size
-    int32_t grid;            // batches per round (= scratch slots)
-    int32_t ldsBytes;        // k_batch_relax dynamic LDS
+    int32_t grid;            // resident workgroups (= scratch slots)
+    int32_t ldsBytes;
     double delta;            // bucket width
-    double bucketWidth;      // distance-bucket level width (< min arc latency), 0 = off
 };
 
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)

@@ -146,7 +146,6 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_THREADS", t.batchThreads);
     gi("SHDPE_BATCH_GRID", t.batchGrid);
     gi("SHDPE_BATCH_ORDER", t.batchOrder);
-    gi("SHDPE_BATCH_BUCKET_LEVELS", t.batchBucketLevels);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -267,12 +266,18 @@ static int configure(ShdPe* pe, Shard* sh) {
     b.ldsBytes = batch_lds_bytes((int)n);
     if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
-    b.grid = 0;                       // batches per round: ensure_batch (memory budget)
+    int bPerCU = 1;
+    if (b.ldsBytes <= LDS &&
+        (hipFuncSetAttribute(batch_kernel_ptr(b.lb), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             b.ldsBytes) != hipSuccess ||
+         hipOccupancyMaxActiveBlocksPerMultiprocessor(&bPerCU, batch_kernel_ptr(b.lb), b.threads,
+                                                      b.ldsBytes) != hipSuccess ||
+         bPerCU < 1))
+        bPerCU = 1;
+    b.grid = sh->numCUs * bPerCU;
+    if (tu.batchGrid > 0 && tu.batchGrid < b.grid) b.grid = tu.batchGrid;
     b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
     if (!(b.delta > 0)) b.delta = 1.0;
-    // hops / reliability by distance-bucket levels (pe_batch.hip): width just
-    // under the smallest arc latency; SHDPE_BATCH_BUCKET_LEVELS=0 disables
-    b.bucketWidth = tu.batchBucketLevels && g.minArcLatency > 0.0 ? g.minArcLatency * 0.999 : 0.0;
     sh->bcfg = b;
     sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
     sh->stats.batched = pe->batched ? 1 : 0;
@@ -611,22 +616,18 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     const size_t LB = (size_t)sh->bcfg.lb;
     const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4;
-    // scratch budget (default 64 GiB) -> slots = batches per round; rounds
-    // of equal size (a short last round would leave CUs idle)
+    // scratch budget (default 64 GiB): fewer resident batches on huge graphs
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
-    size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
-    if (pe->tu.batchGrid > 0) maxSlots = std::min<size_t>(maxSlots, (size_t)pe->tu.batchGrid);
-    const size_t nBatchesAll = std::max<size_t>(1, ((size_t)sh->rowCount + LB - 1) / LB);
-    const size_t rounds = (nBatchesAll + maxSlots - 1) / maxSlots;
-    const size_t slots = (nBatchesAll + rounds - 1) / rounds;
+    const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
+    const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
+    const size_t slots = std::min<size_t>({(size_t)sh->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
     sh->bcfg.grid = (int32_t)slots;
     int rc;
-    void *D, *R, *H, *P, *X, *q, *info, *rows, *amb;
+    void *D, *R, *H, *P, *X, *q, *rows, *amb;
     if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &X, slots * NS * LB * 16)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
         (rc = dev_alloc(sh, &q, slots * NS * 4)) ||
-        (rc = dev_alloc(sh, &info, (nBatchesAll + 64) * 16)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
         (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)))
         return rc;
@@ -636,7 +637,6 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.P = (int32_t*)P;
     sh->bsc.X = (int32_t*)X;
     sh->bsc.queue = (int32_t*)q;
-    sh->bsc.info = info;
     sh->bsc.nStride = (int64_t)NS;
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
@@ -684,7 +684,7 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
     long rnd = 0, dmax = 0, ambB = 0, rep = 0;
     double tMin = 1e30, tMax = 0, tSum = 0, tSq = 0;
     for (int32_t i = 0; i < nB; ++i) {
-        const int32_t* d = d0 + 32 * i;
+        const int32_t* d = d0 + 16 * i;
         ph += d[0]; rnd += d[1]; dmax = std::max<long>(dmax, d[2]);
         ambB += d[3] != 0;
         rep += d[15];
@@ -700,12 +700,6 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
     }
     const double mean = tSum / std::max(nB, 1);
     const double sd = std::sqrt(std::max(0.0, tSq / std::max(nB, 1) - mean * mean));
-    double lw = 0, ln = 0, lsc = 0;
-    for (int32_t i = 0; i < nB; ++i) {
-        lw += d0[32 * i + 16]; ln += d0[32 * i + 19]; lsc += 1024.0 * d0[32 * i + 20];
-    }
-    std::fprintf(stderr, "[shdpe] level loop entries/batch=%.0f levels=%.1f | scatter Mcycles/batch=%.2f (in rel)\n",
-                 lw / nB, ln / nB, lsc / nB / 1e6);
     std::fprintf(stderr, "[shdpe] shard %d batch relax Mcycles/batch: sum over phases of group-busy max=%.2f mean=%.2f | candidates/batch=%.0f\n",
                  sh->gindex, bmax / nB / 1e6, bmean / nB / 1e6, cand / nB);
     std::fprintf(stderr, "[shdpe] batch arc-visits/batch=%.0f (%.2f x nArcs) active lanes/proc=%.2f\n",
@@ -803,7 +797,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             order.resize((size_t)nB * LB, -1);
             HIPCHK(hipMemcpyAsync(sh->dBatchRows, order.data(), order.size() * 4,
                                   hipMemcpyHostToDevice, sh->stream));
-            if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 128, sh->stream));
+            if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 64, sh->stream));
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
                               sh->dDbg, sh->stream);
@@ -818,7 +812,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             for (size_t i = 0; i < order.size(); ++i)
                 if (order[i] >= 0 && amb[i]) exactRows.push_back(order[i]);
             if (sh->dDbg) {
-                std::vector<int32_t> dbg((size_t)nB * 32);
+                std::vector<int32_t> dbg((size_t)nB * 16);
                 HIPCHK(hipMemcpy(dbg.data(), sh->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
                 print_batch_debug(pe, sh, dbg.data(), nB);
             }

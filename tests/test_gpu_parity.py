@@ -355,7 +355,7 @@ def _chain(n, seed, vloss=False):
                     rng.uniform(0.0, 0.01, n) if vloss else None)
 
 
-@pytest.mark.parametrize("n,vloss", [(4400, False), (300, True)])
+@pytest.mark.parametrize("n,vloss", [(4400, False), (300, True), (1500, True)])
 def test_batched_kernel_deep_trees(E, oracle_mod, n, vloss):
     """Deep predecessor trees in k_batch_rows: many pointer-jumping rounds,
     depth > LMAX (4096: Gauss-Seidel reliability sweeps) and, with vertex
