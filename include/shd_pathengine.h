@@ -130,6 +130,9 @@ typedef struct ShdPeStats {
     int32_t batchLanes;        /* sources per batch (LB) when batched              */
     int32_t nShards;           /* row shards (devices) in this engine              */
     double msGather;           /* device time of shd_pe_gather                     */
+    int64_t rowsTieEarly;      /* of rowsExact: early-stop emulation (the batch
+                                  kernel exported distances, parents and the tie
+                                  threshold; k_tie_write wrote the row)          */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */

@@ -121,8 +121,11 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                                                            BatchScratch bs,
                                                            const int32_t* __restrict__ batchRows,
                                                            int32_t nBatches, uint8_t* rowAmbig,
-                                                           double delta, int32_t* dbg) {
+                                                           double delta, int32_t* dbg,
+                                                           const TieBuf* __restrict__ tieDesc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int tieSlot[LB];
+    __shared__ unsigned long long tieThr[LB];
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     constexpr unsigned int LBMASK = LB >= 32 ? 0xFFFFFFFFu : ((1u << (LB & 31)) - 1u);
@@ -439,7 +442,6 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                             const unsigned long long cb = d2b(cand);
                             mn[v] = cb < mn[v] ? cb : mn[v];
                             if (dvb[v] != INF_BITS && du[v][k] <= dvb[v] && cand == b2d(dvb[v])) {
-                                if (du[v][k] == dvb[v]) amb = true;   // zero-increment arc
                                 if (du[v][k] < best[v]) {
                                     best[v] = du[v][k];
                                     cnt[v] = 1;
@@ -464,7 +466,17 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
                     if (bm && l == 0) atomicOr(&anyC[vv >> 5], 1u << (vv & 31));
                     const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
-                    if (!root[v] && dvb[v] != INF_BITS && cnt[v] != 1) amb = true;
+                    // an entry whose parent the heap decides: equal minimum
+                    // tight predecessors, or the minimum one reaches v by a
+                    // zero-increment arc (dist[u] + w == dist[u]: u and v
+                    // share a key).  A zero-increment arc from a farther
+                    // predecessor cannot win (its relaxation is not strictly
+                    // better).  Marked in H (free until the hop counts) for
+                    // the tie export below.
+                    const bool ea = !root[v] && dvb[v] != INF_BITS &&
+                                    (cnt[v] != 1 || best[v] == dvb[v]);
+                    amb |= ea;
+                    H[e] = ea ? 1 : 0;
                     P[e] = tree ? ba[v] : -1;
                     st_jh(&JH[e], tree ? bu[v] : vv, tree ? 1 : 0);
                 }
@@ -485,6 +497,55 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         if (!anyViol || failed) break;
         ++repairs;
         }   // verification loop
+        // ---- tie export: rows whose parents the igraph heap decides go to
+        // k_exact_rows; hand it the final distances, these parents and the
+        // ambiguous entries, so it emulates the heap only until the last
+        // tied predecessor is popped (tie threshold) ----
+        if (ambMask && !failed && tieDesc) {
+            // descriptor read from memory here only: as a kernel argument
+            // it cost the hot loops registers (SGPR spills)
+            const TieBuf tie = *tieDesc;
+            if (tid < LB) {
+                int sl = -1;
+                if ((ambMask >> tid) & 1u) {
+                    sl = atomicAdd(tie.count, 1);
+                    if (sl >= tie.cap) sl = -1;
+                }
+                tieSlot[tid] = sl;
+                tieThr[tid] = 0ull;
+            }
+            __syncthreads();
+            const int sl = tieSlot[l];
+            unsigned long long thr = 0ull;
+            for (int v = gid; v < n; v += NG) {
+                if (sl < 0) continue;
+                const size_t e = (size_t)v * LB + l;
+                const int am = ld_wg(&H[e]);
+                const size_t o = (size_t)sl * (size_t)tie.n + v;
+                tie.D[o] = b2d(ld_wg(&D[e]));
+                tie.P[o] = ld_wg(&P[e]) | (am ? TIE_AMB : 0);
+                if (am) {   // rare: re-derive the tied (minimum tight) predecessor distance
+                    const unsigned long long dv = ld_wg(&D[e]);
+                    const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];
+                    const int a1 = undirected ? g.rowPtr[v + 1] : g.inPtr[v + 1];
+                    unsigned long long mt = INF_BITS;
+                    for (int a = a0; a < a1; ++a) {
+                        const int u = undirected ? g.col[a] : g.inCol[a];
+                        const double w = undirected ? g.lat[a] : g.inLat[a];
+                        const unsigned long long du = ld_wg(&D[(size_t)u * LB + l]);
+                        if (du <= dv && d2b(b2d(du) + w) == dv && du < mt) mt = du;
+                    }
+                    if (mt != INF_BITS) thr = mt > thr ? mt : thr;
+                }
+            }
+            if (thr) atomicMax(&tieThr[l], thr);
+            fence_wg();
+            __syncthreads();
+            if (gid == 0 && sl >= 0) tie.thr[sl] = b2d(tieThr[l]);
+        } else if (tid < LB) {
+            tieSlot[tid] = -1;
+        }
+        __syncthreads();
         const long long tPh2 = dbg ? (long long)clock64() : 0;
 
         // ================= 3. hop counts: pointer jumping ====================
@@ -663,7 +724,11 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         }
         const long long tPh4 = dbg ? (long long)clock64() : 0;
         if (failed) ambMask = LBMASK;     // hand every row to k_exact_rows
-        if (gid == 0 && row >= 0) rowAmbig[(size_t)b * LB + l] = (ambMask >> l) & 1u;
+        // 0 fast path, 1 full igraph-heap emulation, 2 + slot: early-stop
+        // emulation with the exported tie data
+        if (gid == 0 && row >= 0)
+            rowAmbig[(size_t)b * LB + l] =
+                ((ambMask >> l) & 1u) ? (uint8_t)(tieSlot[l] >= 0 ? 2 + tieSlot[l] : 1) : (uint8_t)0;
         if (dbg && tid == 0) {
             dbg[16 * b + 0] = phases;
             dbg[16 * b + 1] = rounds;
@@ -736,11 +801,12 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
 template <int LB>
 static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
-                      const BatchLaunch& cfg, int32_t* dDbg, hipStream_t st, int grid) {
+                      const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st,
+                      int grid) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
     hipLaunchKernelGGL(k_batch_rows<LB>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
-                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg);
+                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
 }
 
 int batch_lds_bytes(int n) {
@@ -756,16 +822,16 @@ const void* batch_kernel_ptr(int lb) {
 
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
-                       const BatchLaunch& cfg, int32_t* dDbg, void* stream) {
+                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream) {
     if (nBatches <= 0) return;
     const int grid = nBatches < cfg.grid ? nBatches : cfg.grid;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (cfg.lb == 8)
-        launch_lb<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st, grid);
+        launch_lb<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (cfg.lb == 32)
-        launch_lb<32>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st, grid);
+        launch_lb<32>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else
-        launch_lb<16>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, st, grid);
+        launch_lb<16>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
 }
 
 }  // namespace shdpe

@@ -123,6 +123,22 @@ struct BatchLaunch {
     double delta;            // bucket width
 };
 
+// Tie export (pe_batch.hip -> k_exact_rows early stop -> k_tie_write): per
+// slot the final distances, the fast-path parents (IN-arc index) with
+// TIE_AMB marking entries whose parent the igraph heap decides, and the
+// largest tied predecessor distance (the emulation stops past it).
+constexpr int32_t TIE_AMB = 1 << 30;
+struct TieBuf {
+    int32_t cap;             // slots (<= 254: rowAmbig holds 2 + slot)
+    int32_t* count;          // device slot counter (reset per launch)
+    double* D;               // [cap][n]
+    int32_t* P;              // [cap][n]
+    double* thr;             // [cap]
+    int32_t* H;              // [cap][n] k_tie_write hop labels
+    double* R;               // [cap][n] k_tie_write reliability labels
+    int64_t n;
+};
+
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)
 constexpr uint8_t F_UNREACHABLE = 0x01;
 constexpr uint8_t F_NOEDGE = 0x02;
@@ -147,18 +163,28 @@ struct SparseLaunch {
 void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
                         const SparseLaunch& cfg, int32_t* dDbg, void* stream);
+// dSlots (may be null): per exact row its tie slot (-1 = full emulation);
+// rows with a slot stop at the slot's threshold and leave their final
+// parents in tie.P for launch_tie_write
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
-                       bool ldsIndex, bool forceGlobalHeap, void* stream);
+                       bool ldsIndex, bool forceGlobalHeap, const int32_t* dSlots,
+                       const TieBuf& tie, void* stream);
+// rows (dRows) with their tie slots (dSlots): hops / reliability along the
+// final parents, row writer
+void launch_tie_write(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
+                      const int32_t* dSlots, int32_t nRows, const TieBuf& tie, void* stream);
 void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
                         int32_t nRows, void* stream);
 int sparse_max_threads();
 // batched multi-source sparse path (pe_batch.hip): batchRows = nBatches*lb
-// table positions (-1 pads a short batch); rowAmbig[i] = 1 when entry i's
-// row has equal-distance predecessor ties (-> k_exact_rows).
+// table positions (-1 pads a short batch); rowAmbig[i] != 0 when entry i's
+// row has equal-distance predecessor ties (-> k_exact_rows): 1 = full heap
+// emulation, 2 + k = tie data exported to slot k of *dTie (device copy of
+// the descriptor; null disables the export).
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
-                       const BatchLaunch& cfg, int32_t* dDbg, void* stream);
+                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream);
 const void* batch_kernel_ptr(int lb);
 int batch_lds_bytes(int n);
 // dense path (pe_dense.hip)

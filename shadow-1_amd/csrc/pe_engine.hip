@@ -67,6 +67,9 @@ struct Shard {
     bool batchReady = false;
     int32_t* dBatchRows = nullptr;
     uint8_t* dBatchAmb = nullptr;
+    TieBuf tie{};                   // early-stop tie rows (batched path)
+    int32_t* dSlots = nullptr;      // per exact row its tie slot, -1 full emulation
+    TieBuf* dTie = nullptr;         // device copy of `tie` (k_batch_rows reads it)
     double *dW = nullptr, *dRl = nullptr, *dD = nullptr;
     int32_t* dP = nullptr;
     uint8_t *dRowA = nullptr, *dRowB = nullptr, *dRowAmbD = nullptr, *dChunkEpoch = nullptr;
@@ -640,6 +643,26 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.nStride = (int64_t)NS;
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
+    // tie slots: D f64 + P i32 + H i32 + R f64 per vertex, <= 2 GiB, <= 254
+    // (rowAmbig stores 2 + slot in a byte); arc indices carry TIE_AMB in bit 30
+    const size_t perTie = (size_t)pe->hg.n * 24;
+    size_t cap = std::min<size_t>({(size_t)254, (size_t)sh->rowsCap, ((size_t)2 << 30) / perTie});
+    if (pe->hg.nArcs() >= ((int64_t)1 << 30)) cap = 0;
+    if (cap > 0) {
+        void *td, *tp, *th, *tr, *tt, *tc, *sl, *dd;
+        const size_t cn = cap * (size_t)pe->hg.n;
+        if ((rc = dev_alloc(sh, &td, cn * 8)) || (rc = dev_alloc(sh, &tp, cn * 4)) ||
+            (rc = dev_alloc(sh, &th, cn * 4)) || (rc = dev_alloc(sh, &tr, cn * 8)) ||
+            (rc = dev_alloc(sh, &tt, cap * 8)) || (rc = dev_alloc(sh, &tc, 16)) ||
+            (rc = dev_alloc(sh, &sl, (size_t)sh->rowsCap * 4)) ||
+            (rc = dev_alloc(sh, &dd, sizeof(TieBuf))))
+            return rc;
+        sh->tie = TieBuf{(int32_t)cap, (int32_t*)tc, (double*)td, (int32_t*)tp, (double*)tt,
+                         (int32_t*)th, (double*)tr, (int64_t)pe->hg.n};
+        sh->dSlots = (int32_t*)sl;
+        sh->dTie = (TieBuf*)dd;
+        HIPCHK(hipMemcpy(sh->dTie, &sh->tie, sizeof(TieBuf), hipMemcpyHostToDevice));
+    }
     sh->batchReady = true;
     return SHD_PE_OK;
 }
@@ -743,7 +766,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
     int rc = ensure_table(pe, sh);
     if (rc) return rc;
     std::vector<uint8_t> amb;
-    std::vector<int32_t> exactRows;
+    std::vector<int32_t> exactRows, exactSlots, fullRows;
     ShdPeStats& st = sh->stats;
     HIPCHK(hipEventRecord(sh->ev0, sh->stream));
     for (int32_t c0 = 0; c0 < count; c0 += sh->rowsCap) {
@@ -751,6 +774,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
         HIPCHK(hipMemcpyAsync(sh->dRows, pos + c0, (size_t)cnt * 4, hipMemcpyHostToDevice,
                               sh->stream));
         exactRows.clear();
+        exactSlots.clear();
         if (pe->mode == 2) {
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_direct_rows(sh->dg, sh->tab, sh->dRows, cnt, sh->stream);
@@ -798,9 +822,10 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             HIPCHK(hipMemcpyAsync(sh->dBatchRows, order.data(), order.size() * 4,
                                   hipMemcpyHostToDevice, sh->stream));
             if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 64, sh->stream));
+            if (sh->tie.cap > 0) HIPCHK(hipMemsetAsync(sh->tie.count, 0, 4, sh->stream));
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
-                              sh->dDbg, sh->stream);
+                              sh->dDbg, sh->dTie, sh->stream);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(sh->evB, sh->stream));
             amb.resize(order.size());
@@ -809,8 +834,24 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             HIPCHK(hipStreamSynchronize(sh->stream));
             st.msSparseKernel += elapsed(sh->evA, sh->evB);
             st.launchesSparse++;
-            for (size_t i = 0; i < order.size(); ++i)
-                if (order[i] >= 0 && amb[i]) exactRows.push_back(order[i]);
+            // early-stop tie rows first (k_tie_write takes that prefix),
+            // then rows needing the full emulation
+            fullRows.clear();
+            for (size_t i = 0; i < order.size(); ++i) {
+                if (order[i] < 0 || !amb[i]) continue;
+                if (amb[i] >= 2) {
+                    exactRows.push_back(order[i]);
+                    exactSlots.push_back(amb[i] - 2);
+                } else {
+                    fullRows.push_back(order[i]);
+                }
+            }
+            if (!exactSlots.empty()) {
+                exactRows.insert(exactRows.end(), fullRows.begin(), fullRows.end());
+                exactSlots.resize(exactRows.size(), -1);
+            } else {
+                exactRows.swap(fullRows);
+            }
             if (sh->dDbg) {
                 std::vector<int32_t> dbg((size_t)nB * 16);
                 HIPCHK(hipMemcpy(dbg.data(), sh->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
@@ -839,11 +880,24 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
         if (!exactRows.empty()) {
             HIPCHK(hipMemcpyAsync(sh->dRows, exactRows.data(), exactRows.size() * 4,
                                   hipMemcpyHostToDevice, sh->stream));
+            const int32_t* dSl = nullptr;
+            int32_t nTie = 0;
+            if (!exactSlots.empty()) {
+                HIPCHK(hipMemcpyAsync(sh->dSlots, exactSlots.data(), exactSlots.size() * 4,
+                                      hipMemcpyHostToDevice, sh->stream));
+                dSl = sh->dSlots;
+                while (nTie < (int32_t)exactSlots.size() && exactSlots[nTie] >= 0) ++nTie;
+            }
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
                               sh->exactGrid, sh->exactHc, sh->exactLdsIdx,
-                              pe->tu.exactHc > 0 || pe->tu.exactAos, sh->stream);
+                              pe->tu.exactHc > 0 || pe->tu.exactAos, dSl, sh->tie, sh->stream);
             HIPCHK(hipGetLastError());
+            if (nTie > 0) {
+                launch_tie_write(sh->dg, sh->tab, sh->dRows, sh->dSlots, nTie, sh->tie, sh->stream);
+                HIPCHK(hipGetLastError());
+                st.rowsTieEarly += nTie;
+            }
             HIPCHK(hipEventRecord(sh->evB, sh->stream));
             HIPCHK(hipEventSynchronize(sh->evB));
             st.msExactKernel += elapsed(sh->evA, sh->evB);
@@ -1370,6 +1424,7 @@ extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
         const ShdPeStats& s = pe->shards[i]->stats;
         t.rowsComputed += s.rowsComputed;
         t.rowsExact += s.rowsExact;
+        t.rowsTieEarly += s.rowsTieEarly;
         t.arcsRelaxed += s.arcsRelaxed;
         t.msSparseKernel += s.msSparseKernel;
         t.msExactKernel += s.msExactKernel;

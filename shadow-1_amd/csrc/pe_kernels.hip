@@ -82,11 +82,20 @@ __device__ __noinline__ double fold_rel_general(const double* __restrict__ vrel,
         for (int i = k - 1; i >= 0; --i) acc = acc * fac[i];
         return acc;
     }
-    // long chains: O(h^2) re-walk, exact order, no scratch
-    for (int d = 1; d <= h; ++d) {
+    // long chains: blocks of 64 factors in source->target order; block k
+    // re-walks the h - hi hops above it (O(h^2 / 64) steps, no scratch)
+    for (int lo = 0; lo < h; lo += 64) {
+        const int hi = h < lo + 64 ? h : lo + 64;
         int x = t;
-        for (int up = 0; up < h - d; ++up) x = inCol[P[x]];
-        acc = acc * inRel[P[x]];
+        for (int up = 0; up < h - hi; ++up) x = inCol[P[x]];
+        double fac[64];
+        int k = 0;
+        while (k < hi - lo) {
+            const int a = P[x];
+            fac[k++] = inRel[a];
+            x = inCol[a];
+        }
+        for (int i = k - 1; i >= 0; --i) acc = acc * fac[i];
     }
     return acc;
 }
@@ -844,6 +853,80 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
 }
 
 // ---------------------------------------------------------------------------
+// Early-stop tie rows.  k_batch_rows exported the final distances and the
+// fast-path parents of a tie row, TIE_AMB marking the entries whose parent
+// the heap decides (equal-minimum tight predecessors / zero-increment arcs),
+// and the largest tied predecessor distance thr.  The igraph heap emulation
+// stops before the first pop with key > thr: by then every tied predecessor
+// was popped, so the emulated parent of each marked entry is final (a later
+// pop never improves its distance strictly).  Unmarked entries have a single
+// candidate parent, which the emulation would pick too.  tie_finalize merges
+// the two parent sets; k_tie_write derives hops / reliability along them.
+// ---------------------------------------------------------------------------
+template <class Reached>
+__device__ __forceinline__ void tie_finalize(const TieBuf& tie, int slot, int n, int lane,
+                                             Reached reached, const int32_t* P) {
+    int32_t* tp = tie.P + (size_t)slot * (size_t)tie.n;
+    for (int v = lane; v < n; v += EX_THREADS) {
+        const int fp = tp[v];
+        if (fp >= 0 && (fp & TIE_AMB))
+            tp[v] = reached(v) ? P[v] : -1;   // unreached: off every target's path
+    }
+}
+
+// One workgroup per tie row: hop counts and reliability products level by
+// level along the final parent tree (level d reads only level d - 1, written
+// before the barrier), then the row writer (topology.c:1805-1864).
+constexpr int TW_THREADS = 1024;
+
+__global__ __launch_bounds__(TW_THREADS) void k_tie_write(DevGraph g0, DevTable tab0,
+                                                          const int32_t* __restrict__ rows,
+                                                          const int32_t* __restrict__ slots,
+                                                          TieBuf tie) {
+    const DevGraph g = global_view(g0);
+    const DevTable tab = global_view(tab0);
+    __shared__ int changed;
+    const int n = g.n;
+    const int tid = threadIdx.x;
+    const int r = rows[blockIdx.x];
+    const int s = g.attached[r];
+    const size_t off = (size_t)slots[blockIdx.x] * (size_t)tie.n;
+    const double* D = tie.D + off;
+    const int32_t* P = tie.P + off;
+    int32_t* H = tie.H + off;
+    double* R = tie.R + off;
+    for (int v = tid; v < n; v += TW_THREADS) {
+        H[v] = v == s ? 0 : -1;
+        R[v] = 1.0;
+    }
+    __syncthreads();
+    if (tid == 0) changed = 0;
+    __syncthreads();
+    for (int d = 1;; ++d) {
+        int ch = 0;
+        for (int v = tid; v < n; v += TW_THREADS) {
+            if (H[v] >= 0) continue;
+            const int a = P[v];
+            if (a < 0) continue;
+            const int x = g.inCol[a];
+            if (H[x] != d - 1) continue;
+            R[v] = R[x] * g.inRel[a];
+            H[v] = d;
+            ch = 1;
+        }
+        if (ch) changed = 1;
+        __syncthreads();
+        const int any = changed;
+        __syncthreads();              // everyone has read it before the reset
+        if (!any) break;
+        if (tid == 0) changed = 0;
+        __syncthreads();
+    }
+    write_row(g, tab, r, s, [&](int t) { return d2b(D[t]); }, [&](int t) { return H[t]; }, R, P,
+              F_EXACT, tid, TW_THREADS);
+}
+
+// ---------------------------------------------------------------------------
 // k_exact_rows: igraph 0.7.1 Dijkstra with the 2-way heap (heap.c), one wave
 // per row.  index2: 0 never reached, 1 popped, >=2 heap position + 2.
 //
@@ -964,7 +1047,9 @@ template <bool LDSIDX>
 __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable tab0,
                                                            DevScratch sc0,
                                                            const int32_t* __restrict__ rows,
-                                                           int32_t nRows, int32_t hc) {
+                                                           int32_t nRows, int32_t hc,
+                                                           const int32_t* __restrict__ slots,
+                                                           TieBuf tie) {
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
@@ -992,6 +1077,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
         const int r = rows[b];
         const int s = g.attached[r];
+        const int tslot = slots ? slots[b] : -1;
+        const double thr = tslot >= 0 ? tie.thr[tslot] : 0.0;
         XHeap<LDSIDX> h{heapGlb, sc.index2 + slot, hc, 0};
         for (int v = lane; v < n; v += EX_THREADS) h.set_idx2(v, 0);
         __syncthreads();
@@ -1018,6 +1105,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                 ru = top.rel;
             }
             u = __builtin_amdgcn_readfirstlane(u);
+            // early stop: every tied predecessor popped, parents final
+            if (tslot >= 0 && __shfl(mind, 0, 64) > thr) break;
             const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
             const int att = g.isAttached[u];
             if (lane == 0) {
@@ -1077,9 +1166,12 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
             if (fence) __syncthreads();
         }
         __syncthreads();
-        write_row(g, tab, r, s,
-                  [&](int t) { return h.idx2(t) == 1 ? d2b(D[t]) : INF_BITS; },
-                  [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
+        if (tslot >= 0)
+            tie_finalize(tie, tslot, n, lane, [&](int v) { return h.idx2(v) != 0; }, P);
+        else
+            write_row(g, tab, r, s,
+                      [&](int t) { return h.idx2(t) == 1 ? d2b(D[t]) : INF_BITS; },
+                      [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
         __syncthreads();
     }
 }
@@ -1096,7 +1188,9 @@ constexpr int EX_SOA_MAXN = 10240;
 __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevTable tab0,
                                                                DevScratch sc0,
                                                                const int32_t* __restrict__ rows,
-                                                               int32_t nRows) {
+                                                               int32_t nRows,
+                                                               const int32_t* __restrict__ slots,
+                                                               TieBuf tie) {
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
@@ -1154,6 +1248,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
         const int r = rows[b];
         const int s = g.attached[r];
+        const int tslot = slots ? slots[b] : -1;
+        const double thr = tslot >= 0 ? tie.thr[tslot] : 0.0;
         for (int v = lane; v < n; v += EX_THREADS) index2[v] = 0;
         if (lane == 0) {
             place(0, 0.0, s);
@@ -1168,6 +1264,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
             // pop: top known before the sift-down, its arc range loads meanwhile
             const int u = __builtin_amdgcn_readfirstlane(hidx[0]);
             const double mind = -hkey[0];
+            if (tslot >= 0 && mind > thr) break;   // early stop (tied preds popped)
             // labels of u were written by lanes of this wave: order their
             // stores, then fetch labels + arc range together (one round trip
             // that overlaps the sift-down)
@@ -1224,9 +1321,12 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
             }
         }
         __syncthreads();
-        write_row(g, tab, r, s,
-                  [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
-                  [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
+        if (tslot >= 0)
+            tie_finalize(tie, tslot, n, lane, [&](int v) { return index2[v] != 0; }, P);
+        else
+            write_row(g, tab, r, s,
+                      [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
+                      [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
         __syncthreads();
     }
 }
@@ -1322,9 +1422,17 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
         launch_sparse_layout<0>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
 }
 
+void launch_tie_write(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
+                      const int32_t* dSlots, int32_t nRows, const TieBuf& tie, void* stream) {
+    if (nRows <= 0) return;
+    hipLaunchKernelGGL(k_tie_write, dim3(nRows), dim3(TW_THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), g, tab, dRows, dSlots, tie);
+}
+
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
-                       bool ldsIndex, bool forceGlobalHeap, void* stream) {
+                       bool ldsIndex, bool forceGlobalHeap, const int32_t* dSlots,
+                       const TieBuf& tie, void* stream) {
     if (nRows <= 0) return;
     if (grid > nRows) grid = nRows;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1333,7 +1441,7 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows_soa),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, sb);
         hipLaunchKernelGGL(k_exact_rows_soa, dim3(grid), dim3(EX_THREADS), sb, st, g, tab, sc,
-                           dRows, nRows);
+                           dRows, nRows, dSlots, tie);
         return;
     }
     const int bytes = (int)(((size_t)24 * hc + (ldsIndex ? (size_t)4 * g.n : 0) + 15) & ~(size_t)15);
@@ -1341,12 +1449,12 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         hipLaunchKernelGGL(k_exact_rows<true>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab,
-                           sc, dRows, nRows, hc);
+                           sc, dRows, nRows, hc, dSlots, tie);
     } else {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         hipLaunchKernelGGL(k_exact_rows<false>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab,
-                           sc, dRows, nRows, hc);
+                           sc, dRows, nRows, hc, dSlots, tie);
     }
 }
 

@@ -62,7 +62,7 @@ class Stats(C.Structure):
                 ("msDenseKernel", C.c_double), ("launchesDense", C.c_int64),
                 ("denseSweeps", C.c_int64), ("denseFlops", C.c_double),
                 ("batched", C.c_int32), ("batchLanes", C.c_int32), ("nShards", C.c_int32),
-                ("msGather", C.c_double)]
+                ("msGather", C.c_double), ("rowsTieEarly", C.c_int64)]
 
 
 class EngineError(RuntimeError):

@@ -343,6 +343,7 @@ def test_batched_kernel(E, oracle_mod, case):
     assert st["mode"] == 1 and st["launchesSparse"] >= 1
     if case == "quantized":
         assert st["rowsExact"] > 0
+        assert st["rowsTieEarly"] > 0      # early-stop emulation + k_tie_write
 
 
 def _chain(n, seed, vloss=False):
@@ -392,3 +393,34 @@ def test_native_graphml_to_engine(E, oracle_mod):
                    top.loss[keep], top.vloss)
     st = _check_engine(E, oracle_mod, cut, att, sources=att[::5])
     assert st["mode"] != 2
+
+
+def _ladder(k, seed, vloss=False, directed=False):
+    """Two chains 0..k-1 and k..2k-1 with rungs i <-> k+i, all latencies 1:
+    every vertex beyond the first rung has equal-distance predecessors, so
+    every row is a tie row with ties at depth up to ~k (long chains for the
+    blocked reliability fold)."""
+    rng = np.random.default_rng(seed)
+    a = np.arange(k - 1)
+    src = np.concatenate([a, a + k, np.arange(k), np.arange(2 * k)])
+    dst = np.concatenate([a + 1, a + 1 + k, np.arange(k) + k, np.arange(2 * k)])
+    m = src.shape[0]
+    return Topology(2 * k, directed, src, dst, np.ones(m), rng.uniform(0.0, 0.02, m),
+                    rng.uniform(0.0, 0.01, 2 * k) if vloss else None)
+
+
+@pytest.mark.parametrize("k,vloss,directed", [(150, True, False), (350, False, False),
+                                              (120, True, True)])
+def test_batched_tie_rows_early_stop(E, oracle_mod, k, vloss, directed):
+    """Every row is a tie row: the batch kernel exports distances, parents and
+    the tie threshold; k_exact_rows stops at the threshold and k_tie_write
+    folds hops / reliability (vertex loss: blocked chain fold beyond 64
+    hops).  2k > 254 rows overflow the tie slots: the rest take the full
+    heap emulation, both must match the oracle."""
+    top = _ladder(k, seed=k, vloss=vloss, directed=directed)
+    att = np.arange(2 * k, dtype=np.int32)
+    st = _check_engine(E, oracle_mod, top, att, force=5)
+    assert st["mode"] == 1 and st["rowsExact"] > 0
+    assert st["rowsTieEarly"] > 0
+    if 2 * k > 254:
+        assert st["rowsTieEarly"] < st["rowsExact"]
