@@ -523,7 +523,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                 const int am = ld_wg(&H[e]);
                 const size_t o = (size_t)sl * (size_t)tie.n + v;
                 tie.D[o] = b2d(ld_wg(&D[e]));
-                tie.P[o] = ld_wg(&P[e]) | (am ? TIE_AMB : 0);
+                const int pe = ld_wg(&P[e]);
+                tie.P[o] = am ? (TIE_AMB | (pe > 0 ? pe : 0)) : pe;
                 if (am) {   // rare: re-derive the tied (minimum tight) predecessor distance
                     const unsigned long long dv = ld_wg(&D[e]);
                     const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];

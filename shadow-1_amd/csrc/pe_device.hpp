@@ -73,7 +73,7 @@ struct DevTable {
 struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
-    int exactHc = 0, exactPerCU = 0, exactAos = 0;
+    int exactHc = 0, exactPerCU = 0;
     int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 0;
     double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
@@ -81,21 +81,14 @@ struct Tuning {
     int debug = 0, streamWgPerCU = 4;
 };
 
-// k_exact_rows heap entry (igraph_2wheap_t data + index, labels alongside)
-struct alignas(8) XEnt {
-    double key;
-    double rel;
-    int32_t idx;
-    int32_t hops;
-};
-
 struct DevScratch {
     double* dist;      // exact kernel: final distance at pop
     int32_t* hops;
     double* rel;
     int32_t* pred;     // IN-arc index of the chosen predecessor edge, -1 none
-    XEnt* heapEnt;     // exact kernel 2-way heap entries at positions >= hc (LDS below)
-    int64_t heapStride;  // entries per slot in heapEnt
+    double* heapTail;  // exact kernel: heap positions >= hc, per slot heapStride keys (f64)
+                       // then heapStride vertex ids (i32) -- 16 B per entry of stride
+    int64_t heapStride;  // heap tail entries per slot
     int32_t* index2;   // exact kernel: 0 never reached, 1 popped, >=2 heap pos+2
     int32_t* queue;    // sparse LAYOUT 3: frontier queues, (stride + hcap) per slot
     int64_t stride;    // elements per slot (>= n)
@@ -166,10 +159,17 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
 // dSlots (may be null): per exact row its tie slot (-1 = full emulation);
 // rows with a slot stop at the slot's threshold and leave their final
 // parents in tie.P for launch_tie_write
+// hc: heap positions held in LDS (k_exact_rows, n > exact_soa_max_n());
+// forceGlobalHeap: k_exact_rows even when the SoA all-LDS kernel would fit
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
-                       bool ldsIndex, bool forceGlobalHeap, const int32_t* dSlots,
-                       const TieBuf& tie, void* stream);
+                       bool forceGlobalHeap, const int32_t* dSlots, const TieBuf& tie,
+                       long long* dXdbg, void* stream);
+int exact_soa_max_n();
+// tie rows whose ambiguous entries lie on no target's path: thr := -1 (the
+// exact kernel then keeps the fast-path parents)
+void launch_tie_scan(const DevGraph& g, const int32_t* dRows, const int32_t* dSlots,
+                     int32_t nRows, const TieBuf& tie, void* stream);
 // rows (dRows) with their tie slots (dSlots): hops / reliability along the
 // final parents, row writer
 void launch_tie_write(const DevGraph& g, const DevTable& tab, const int32_t* dRows,

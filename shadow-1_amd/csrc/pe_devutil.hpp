@@ -66,7 +66,7 @@ __device__ __forceinline__ DevScratch global_view(const DevScratch& s0) {
     s.hops = as_global(s0.hops);
     s.rel = as_global(s0.rel);
     s.pred = as_global(s0.pred);
-    s.heapEnt = as_global(s0.heapEnt);
+    s.heapTail = as_global(s0.heapTail);
     s.index2 = as_global(s0.index2);
     s.queue = as_global(s0.queue);
     return s;

@@ -61,7 +61,6 @@ struct Shard {
     int32_t rowsCap = 0;
     SparseLaunch cfg{};
     int exactGrid = 0, exactHc = 1;
-    bool exactLdsIdx = false;
     BatchLaunch bcfg{};
     BatchScratch bsc{};
     bool batchReady = false;
@@ -70,6 +69,7 @@ struct Shard {
     TieBuf tie{};                   // early-stop tie rows (batched path)
     int32_t* dSlots = nullptr;      // per exact row its tie slot, -1 full emulation
     TieBuf* dTie = nullptr;         // device copy of `tie` (k_batch_rows reads it)
+    long long* dXdbg = nullptr;     // exact-kernel counters (SHD_PE_DEBUG_COUNTERS)
     double *dW = nullptr, *dRl = nullptr, *dD = nullptr;
     int32_t* dP = nullptr;
     uint8_t *dRowA = nullptr, *dRowB = nullptr, *dRowAmbD = nullptr, *dChunkEpoch = nullptr;
@@ -143,7 +143,6 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gd("SHDPE_DELTA_FACTOR", t.deltaFactor);
     gi("SHDPE_EXACT_HC", t.exactHc);
     gi("SHDPE_EXACT_PER_CU", t.exactPerCU);
-    gi("SHDPE_EXACT_AOS", t.exactAos);
     gi("SHDPE_BATCH", t.batch);
     gi("SHDPE_BATCH_LB", t.batchLB);
     gi("SHDPE_BATCH_THREADS", t.batchThreads);
@@ -244,13 +243,13 @@ static int configure(ShdPe* pe, Shard* sh) {
     if (!(c.delta > 0)) c.delta = 1.0;
     c.kflags = tu.kflags;
     sh->cfg = c;
-    // k_exact_rows: index2 (4n) in LDS up to n = 24k, heap entries (24 B)
-    // in LDS up to the budget, the tail of the heap in the global slot.  A
-    // whole heap that fits leaves room for several rows per CU.
-    sh->exactLdsIdx = (size_t)4 * n <= 96 * 1024;
-    const long idxB = sh->exactLdsIdx ? 4 * n : 0;
-    const long perWG = std::min<long>(LDS, idxB + 24 * n + 16);
-    sh->exactHc = (int)std::max<long>(1, std::min<long>(n, (perWG - idxB - 16) / 24));
+    // exact kernels: n <= exact_soa_max_n() keeps heap + index2 wholly in
+    // LDS (16 B per vertex, several rows per CU); larger graphs keep the top
+    // of the heap in LDS (12 B per entry, up to the whole 160 KB) and the
+    // tail in the global slot.
+    const bool soa = n <= exact_soa_max_n() && tu.exactHc <= 0;
+    const long perWG = soa ? 16L * n + 16 : std::min<long>(LDS, 12L * n + 16);
+    sh->exactHc = (int)std::max<long>(1, std::min<long>(n, (std::min<long>(LDS, perWG) - 16) / 12));
     if (tu.exactHc > 0) sh->exactHc = std::min(sh->exactHc, tu.exactHc);   // tests: global heap tail
     const int exPerCU = (int)std::max<long>(1, std::min<long>(8, LDS / perWG));
     sh->exactGrid = sh->numCUs * (tu.exactPerCU > 0 ? tu.exactPerCU : exPerCU);
@@ -581,14 +580,14 @@ static int ensure_table(ShdPe* pe, Shard* sh) {
         (rc = dev_alloc(sh, &sho, slots * stride * 4)) ||
         (rc = dev_alloc(sh, &sr, slots * stride * 8)) ||
         (rc = dev_alloc(sh, &sp, slots * stride * 4)) ||
-        (rc = dev_alloc(sh, &hk, (size_t)sh->exactGrid * heapStride * sizeof(XEnt))) ||
-        (rc = dev_alloc(sh, &i2, sh->exactLdsIdx ? 16 : (size_t)sh->exactGrid * stride * 4)))
+        (rc = dev_alloc(sh, &hk, (size_t)sh->exactGrid * heapStride * 16)) ||
+        (rc = dev_alloc(sh, &i2, (size_t)sh->exactGrid * stride * 4)))
         return rc;
     sh->sc.dist = (double*)dist;
     sh->sc.hops = (int32_t*)sho;
     sh->sc.rel = (double*)sr;
     sh->sc.pred = (int32_t*)sp;
-    sh->sc.heapEnt = (XEnt*)hk;
+    sh->sc.heapTail = (double*)hk;
     sh->sc.heapStride = (int64_t)heapStride;
     sh->sc.index2 = (int32_t*)i2;
     sh->sc.stride = (int64_t)stride;
@@ -609,6 +608,9 @@ static int ensure_table(ShdPe* pe, Shard* sh) {
         void* dbg;
         if ((rc = dev_alloc(sh, &dbg, (size_t)sh->rowsCap * 64))) return rc;
         sh->dDbg = (int32_t*)dbg;
+        void* xd;
+        if ((rc = dev_alloc(sh, &xd, (size_t)sh->rowsCap * 64))) return rc;
+        sh->dXdbg = (long long*)xd;
     }
     sh->tableReady = true;
     return SHD_PE_OK;
@@ -759,6 +761,20 @@ static void print_sparse_debug(ShdPe* pe, Shard* sh, const int32_t* dbg, int32_t
     (void)pe;
 }
 
+// k_exact_rows counters: per row pops, pushes and cycles per pop segment.
+static void print_exact_debug(Shard* sh, const std::vector<int32_t>& rows, int32_t nTie) {
+    std::vector<long long> x(rows.size() * 8);
+    if (hipMemcpy(x.data(), sh->dXdbg, x.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    for (size_t i = 0; i < rows.size(); ++i) {
+        const long long* c = &x[i * 8];
+        const double p = (double)std::max<long long>(c[5], 1);
+        std::fprintf(stderr, "[shdpe] exact row %d (%s): pops=%lld pushes+mods=%lld heap_end=%lld | "
+                     "cyc/pop top=%.0f sink=%.0f arcs=%.0f push=%.0f fence=%.0f total=%.0f\n",
+                     rows[i], (int32_t)i < nTie ? "early" : "full", c[5], c[6], c[7], c[0] / p,
+                     c[1] / p, c[2] / p, c[3] / p, c[4] / p, (c[0] + c[1] + c[2] + c[3] + c[4]) / p);
+    }
+}
+
 // Compute the given table positions (all owned by `sh`), chunked.
 static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count) {
     if (count <= 0) return SHD_PE_OK;
@@ -889,9 +905,10 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 while (nTie < (int32_t)exactSlots.size() && exactSlots[nTie] >= 0) ++nTie;
             }
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
+            if (nTie > 0) launch_tie_scan(sh->dg, sh->dRows, sh->dSlots, nTie, sh->tie, sh->stream);
             launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
-                              sh->exactGrid, sh->exactHc, sh->exactLdsIdx,
-                              pe->tu.exactHc > 0 || pe->tu.exactAos, dSl, sh->tie, sh->stream);
+                              sh->exactGrid, sh->exactHc, pe->tu.exactHc > 0, dSl, sh->tie,
+                              sh->dXdbg, sh->stream);
             HIPCHK(hipGetLastError());
             if (nTie > 0) {
                 launch_tie_write(sh->dg, sh->tab, sh->dRows, sh->dSlots, nTie, sh->tie, sh->stream);
@@ -902,6 +919,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             HIPCHK(hipEventSynchronize(sh->evB));
             st.msExactKernel += elapsed(sh->evA, sh->evB);
             st.launchesExact++;
+            if (sh->dXdbg && pe->hg.n > 10240) print_exact_debug(sh, exactRows, nTie);
             st.rowsExact += (int64_t)exactRows.size();
         }
     }

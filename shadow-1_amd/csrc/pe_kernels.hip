@@ -874,6 +874,48 @@ __device__ __forceinline__ void tie_finalize(const TieBuf& tie, int slot, int n,
     }
 }
 
+// One workgroup per tie row: is any ambiguous entry on the path to a target?
+// A target's igraph path equals its fast-path parent chain up to the first
+// ambiguous vertex on it, so if no target chain meets one the fast-path
+// parents are exact and the emulation is skipped (thr := -1).  tie.H marks
+// vertices whose chain up to the source is known clean (k_tie_write
+// re-initialises it).
+__global__ __launch_bounds__(1024) void k_tie_scan(DevGraph g0, const int32_t* __restrict__ rows,
+                                                   const int32_t* __restrict__ slots, TieBuf tie) {
+    const DevGraph g = global_view(g0);
+    __shared__ int hit;
+    const int n = g.n, T = g.T;
+    const int tid = threadIdx.x;
+    const int s = g.attached[rows[blockIdx.x]];
+    const int sl = slots[blockIdx.x];
+    const size_t off = (size_t)sl * (size_t)tie.n;
+    const int32_t* P = tie.P + off;
+    int32_t* clean = tie.H + off;
+    for (int v = tid; v < n; v += 1024) clean[v] = 0;
+    if (tid == 0) hit = 0;
+    __syncthreads();
+    for (int j = tid; j < T; j += 1024) {
+        if (ld_wg(&hit)) break;
+        const int t = g.attached[j];
+        int x = t, bad = 0;
+        while (x != s && !ld_wg(&clean[x])) {
+            const int p = P[x];
+            if (p < 0) break;                          // unreachable
+            if (p & TIE_AMB) { bad = 1; break; }
+            x = g.inCol[p];
+        }
+        if (bad) { hit = 1; break; }
+        for (int y = t; y != x;) {                     // the walked prefix is clean
+            const int p = P[y];
+            if (p < 0) break;
+            clean[y] = 1;
+            y = g.inCol[p];
+        }
+    }
+    __syncthreads();
+    if (tid == 0 && !hit) tie.thr[sl] = -1.0;
+}
+
 // One workgroup per tie row: hop counts and reliability products level by
 // level along the final parent tree (level d reads only level d - 1, written
 // before the barrier), then the row writer (topology.c:1805-1864).
@@ -928,98 +970,162 @@ __global__ __launch_bounds__(TW_THREADS) void k_tie_write(DevGraph g0, DevTable 
 
 // ---------------------------------------------------------------------------
 // k_exact_rows: igraph 0.7.1 Dijkstra with the 2-way heap (heap.c), one wave
-// per row.  index2: 0 never reached, 1 popped, >=2 heap position + 2.
+// per row, for graphs whose heap does not fit LDS (n > EX_SOA_MAXN).
 //
-// The heap is an array of 24-B entries {key, rel, idx, hops} (the labels
-// ride along, so a pop needs no label gather); positions < hc live in LDS,
-// the rest in the workgroup's global slot.  Lane 0 owns the heap and moves
-// a hole instead of swapping (sift-down/up with the moving key in a
-// register: one LDS round trip per level); the end state is identical to
-// igraph's swap-based igraph_i_2wheap_sink / _shift_up, so the pop order is
-// too.  The wave pre-checks all arcs of the popped vertex in parallel (the
-// decision for arc k depends only on v_k's own state: no parallel edges, no
-// self-loops in the CSR), writes the labels, and lane 0 then applies the
-// pushes / modifies serially in incidence order.  rowPtr of the next top is
-// fetched before the pop's sift-down.
+// Layout: the heap is structure-of-arrays, key f64 (igraph's -dist) + vertex
+// i32; positions < hc in LDS (12 B each: 13.6k entries in 160 KB, the top
+// 13 levels), the tail in the workgroup's global slot.  Per vertex (global):
+// index2 (0 never reached, 1 popped, >= 2 heap position + 2), the current
+// tentative distance (= final distance once popped), labels P/H/R.
+//
+// The heap operations are wave-parallel but leave exactly igraph's array
+// (hence its pop order):
+//   sink     (igraph_i_2wheap_sink): the 62 nodes of the 5-level subtree
+//            below the hole are loaded at once (one lane each); every lane
+//            decides whether it is the child its parent descends to (left
+//            when left >= right or no right), a ballot gives the descent
+//            path, and the moving key passes the path nodes it is strictly
+//            smaller than (a prefix: keys fall along the path).  Those nodes
+//            move up one level in parallel; a full 5-level prefix continues
+//            below.  A 16-level heap costs 4 dependent rounds, not 16.
+//   shift_up (igraph_i_2wheap_shift_up): lane j loads the ancestor j + 1
+//            levels up; the key rises past every ancestor it is not strictly
+//            smaller than (a prefix: keys grow towards the root); those
+//            ancestors move down one level in parallel.
+//   modify   (new key > old key, since igraph modifies only on a strictly
+//            shorter distance): its sink is a no-op, so shift_up alone.
+// The wave pre-checks all arcs of the popped vertex in parallel against
+// index2 / the tentative distance (the decision for arc k depends only on
+// v_k's own state: no parallel edges, no self-loops in the CSR), writes the
+// labels, and the pushes / modifies then run in incidence order.
+// A wave's own global stores are seen by its later loads (wavefront-scope
+// ordering), so heap operations chain without fences.
 // ---------------------------------------------------------------------------
-static_assert(sizeof(XEnt) == 24, "heap entry");
 
 // Heap storage: positions < hc in LDS (dynamic shared memory at offset 0,
 // addressed through the __shared__ symbol so accesses stay ds_* -- a flat
 // access would also wait for every outstanding global store), the tail in
-// the global slot.  index2 in LDS after the heap (LDSIDX) or global.
+// the global slot.
 extern __shared__ __attribute__((aligned(16))) unsigned char ex_smem[];
 
-template <bool LDSIDX>
-struct XHeap {
-    XEnt* glb;        // global tail (position p >= hc at glb[p - hc])
-    int32_t* gidx;    // global index2 (!LDSIDX)
+struct WHeap {
+    double* gkey;     // global tail: position p >= hc at gkey[p - hc]
+    int32_t* gidx;
+    int32_t* I2;      // index2 (global, per vertex)
     int hc;
-    int size;
+    __device__ __forceinline__ double* lkey() const { return reinterpret_cast<double*>(ex_smem); }
     __device__ __forceinline__ int32_t* lidx() const {
-        return reinterpret_cast<int32_t*>(ex_smem + (size_t)24 * hc);
+        return reinterpret_cast<int32_t*>(ex_smem + (size_t)8 * hc);
     }
-    __device__ __forceinline__ int32_t idx2(int v) const { return LDSIDX ? lidx()[v] : gidx[v]; }
-    __device__ __forceinline__ void set_idx2(int v, int x) const {
-        if (LDSIDX) lidx()[v] = x; else gidx[v] = x;
-    }
-    // any lane (pre-check): LDS read always, global only for tail positions
-    __device__ __forceinline__ double key(int p) const {
-        if (p < hc) return reinterpret_cast<const XEnt*>(ex_smem)[p].key;
-        double k = glb[p - hc].key;
-        asm volatile("" : "+v"(k));
-        return k;
-    }
-    // lane 0 only: p is made scalar so the LDS/global choice is a uniform
-    // branch (a per-lane select would become one flat access)
-    __device__ __forceinline__ XEnt load(int p) const {
-        p = __builtin_amdgcn_readfirstlane(p);
-        if (p < hc) return reinterpret_cast<const XEnt*>(ex_smem)[p];
-        XEnt e = glb[p - hc];
-        asm volatile("" : "+v"(e.key));   // keeps the two loads apart (no flat merge)
-        return e;
-    }
-    __device__ __forceinline__ void place(int p, const XEnt& e) const {
-        p = __builtin_amdgcn_readfirstlane(p);
+    // per-lane load / store of position p (LDS or global by lane)
+    __device__ __forceinline__ void get(int p, double& k, int& id) const {
         if (p < hc) {
-            reinterpret_cast<XEnt*>(ex_smem)[p] = e;
+            k = lkey()[p];
+            id = lidx()[p];
+            asm volatile("" : "+v"(k), "+v"(id));   // no merge of the two branches
+        } else {                                      // into one flat load
+            k = gkey[p - hc];
+            id = gidx[p - hc];
+            asm volatile("" : "+v"(k), "+v"(id));
+        }
+    }
+    __device__ __forceinline__ void put(int p, double k, int id) const {
+        if (p < hc) {
+            lkey()[p] = k;
+            lidx()[p] = id;
         } else {
-            glb[p - hc] = e;
-            asm volatile("" ::: "memory");
+            gkey[p - hc] = k;
+            gidx[p - hc] = id;
         }
-        set_idx2(e.idx, p + 2);
+        I2[id] = p + 2;
     }
-    // igraph_i_2wheap_sink: go left when left >= right (or no right child),
-    // move only if the moving key is strictly smaller.  Returns the hole.
-    __device__ __forceinline__ int sink_hole(int head, double k) const {
-        for (;;) {
-            const int l = 2 * head + 1, r = l + 1;
-            if (l >= size) return head;
-            const XEnt L = load(l);
-            const bool hasR = r < size;
-            const XEnt R = load(hasR ? r : l);
-            const bool useL = !hasR || L.key >= R.key;
-            XEnt C;
-            C.key = useL ? L.key : R.key;
-            C.rel = useL ? L.rel : R.rel;
-            C.idx = useL ? L.idx : R.idx;
-            C.hops = useL ? L.hops : R.hops;
-            if (!(k < C.key)) return head;
-            place(head, C);
-            head = useL ? l : r;
-        }
+    // LDS-only variants for operations whose positions all lie below hc
+    // (uniform check): no per-lane LDS/global branches
+    __device__ __forceinline__ void put_lds(int p, double k, int id) const {
+        lkey()[p] = k;
+        lidx()[p] = id;
+        I2[id] = p + 2;
     }
-    // igraph_i_2wheap_shift_up: rise unless strictly smaller than the parent
-    // (equal keys rise above existing ones).
-    __device__ __forceinline__ void shift_up_place(int elem, const XEnt& e) const {
-        while (elem > 0) {
-            const int p = ((elem + 1) >> 1) - 1;
-            const XEnt P = load(p);
-            if (e.key < P.key) break;
-            place(elem, P);
-            elem = p;
+    // One round of igraph_i_2wheap_sink of (k, id): the hole at `head` (heap
+    // level hl) and up to 5 levels below it.  Returns true once (k, id) is
+    // placed; otherwise the hole moved `dd` levels down.  Rounds are cut at
+    // the deepest all-LDS level when the rest of the heap then fits one
+    // round, so a sift-down touches the global tail once.
+    __device__ __forceinline__ bool sink_round(int& head, int& hl, double k, int id, int size,
+                                               int ldsLevel, int lane) const {
+        const int bottom = 31 - __builtin_clz(size);       // deepest heap level
+        int dd = bottom - hl < 5 ? bottom - hl : 5;
+        if (dd <= 0) {
+            if (lane == 0) put(head, k, id);
+            return true;
         }
-        place(elem, e);
+        if (hl < ldsLevel && hl + dd > ldsLevel && hl + dd < bottom && bottom - ldsLevel <= 5)
+            dd = ldsLevel - hl;
+        const int q = lane + 2;                            // subtree node (BFS index, root 1)
+        const int d = 31 - __builtin_clz(q);               // its depth below the hole
+        const int pos = (head + 1) * (1 << d) - 1 + (q - (1 << d));
+        const bool left = (q & 1) == 0;
+        const bool valid = d <= dd && pos < size;
+        const bool sibValid = d <= dd && (left ? pos + 1 : pos - 1) < size;
+        const bool lds = (head + 1) * (1 << dd) + (1 << dd) - 2 < hc;   // deepest node of the round
+        double kq = 0.0;
+        int iq = -1;
+        if (lds) {
+            if (valid) { kq = lkey()[pos]; iq = lidx()[pos]; }
+        } else if (valid) {
+            get(pos, kq, iq);
+        }
+        const double ks = __shfl_xor(kq, 1, 64);           // sibling (lanes 2i, 2i+1)
+        // the child its parent descends to: left when left >= right or no right
+        const bool chosen = valid && (left ? (!sibValid || kq >= ks) : !(ks >= kq));
+        const unsigned long long cm = __ballot(chosen);
+        // descent path (scalar): from the hole, the chosen child per level
+        unsigned long long path = 0ull;
+        for (int x = 1, lv = 0; lv < dd; ++lv) {
+            const int c = 2 * x;                           // left child's node index
+            if ((cm >> (c - 2)) & 1ull) x = c;
+            else if ((cm >> (c - 1)) & 1ull) x = c + 1;
+            else break;
+            path |= 1ull << (x - 2);
+        }
+        const bool mv = ((path >> lane) & 1ull) && k < kq;   // passed: a prefix of the path
+        const unsigned long long mm = __ballot(mv);
+        if (mv) {
+            if (lds) put_lds((pos - 1) >> 1, kq, iq);
+            else put((pos - 1) >> 1, kq, iq);
+        }
+        if (mm == 0ull) {
+            if (lane == 0) put(head, k, id);
+            return true;
+        }
+        const int hp = __shfl(pos, 63 - __builtin_clzll(mm), 64);   // deepest node passed
+        if (__builtin_popcountll(mm) < dd) {
+            if (lane == 0) put(hp, k, id);
+            return true;
+        }
+        head = hp;
+        hl += dd;
+        return false;
+    }
+    // igraph_i_2wheap_shift_up of (k, id) from the hole at `elem`
+    __device__ __forceinline__ void shift_up(int elem, double k, int id, int lane) const {
+        const int a = lane < 31 ? ((elem + 1) >> (lane + 1)) - 1 : -1;
+        const bool valid = a >= 0;
+        const bool lds = elem < hc;                      // every ancestor and the hole
+        double ka = 0.0;
+        int ia = -1;
+        if (lds) {
+            if (valid) { ka = lkey()[a]; ia = lidx()[a]; }
+        } else if (valid) {
+            get(a, ka, ia);
+        }
+        const unsigned long long sm = __ballot(!valid || k < ka);
+        const int c = __builtin_ctzll(sm);               // ancestors passed
+        if (lane < c) {
+            if (lds) put_lds(((elem + 1) >> lane) - 1, ka, ia);
+            else put(((elem + 1) >> lane) - 1, ka, ia);
+        }
+        if (lane == 0) put(c == 0 ? elem : ((elem + 1) >> c) - 1, k, id);
     }
 };
 
@@ -1043,26 +1149,24 @@ __device__ __forceinline__ uint32_t warm_cache(const void* p, size_t bytes, int 
     return acc;
 }
 
-template <bool LDSIDX>
 __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable tab0,
                                                            DevScratch sc0,
                                                            const int32_t* __restrict__ rows,
                                                            int32_t nRows, int32_t hc,
                                                            const int32_t* __restrict__ slots,
-                                                           TieBuf tie) {
+                                                           TieBuf tie, long long* xdbg) {
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
     const int n = g.n;
     const int lane = threadIdx.x;
     const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
-    XEnt* heapGlb = sc.heapEnt + (size_t)blockIdx.x * (size_t)sc.heapStride;
-    double* D = sc.dist + slot;
+    double* D = sc.dist + slot;          // tentative distance; final once popped
     int32_t* H = sc.hops + slot;
     double* R = sc.rel + slot;
     int32_t* P = sc.pred + slot;
-    // heap and index2 wholly in LDS: one wave, in-order LDS -> no fences
-    const bool fence = !LDSIDX || hc < n;
+    double* tailKey = reinterpret_cast<double*>(sc.heapTail) + (size_t)blockIdx.x * 2 * sc.heapStride;
+    const WHeap h{tailKey, reinterpret_cast<int32_t*>(tailKey + sc.heapStride), sc.index2 + slot, hc};
     {
         const size_t m = (size_t)g.rowPtr[n];
         uint32_t acc = warm_cache(g.rowPtr, (size_t)4 * (n + 1), lane, EX_THREADS);
@@ -1079,103 +1183,126 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
         const int s = g.attached[r];
         const int tslot = slots ? slots[b] : -1;
         const double thr = tslot >= 0 ? tie.thr[tslot] : 0.0;
-        XHeap<LDSIDX> h{heapGlb, sc.index2 + slot, hc, 0};
-        for (int v = lane; v < n; v += EX_THREADS) h.set_idx2(v, 0);
+        if (tslot < 0 || thr >= 0.0)
+            for (int v = lane; v < n; v += EX_THREADS) h.I2[v] = 0;
         __syncthreads();
         if (lane == 0) {
-            h.size = 1;
-            h.place(0, XEnt{0.0, 1.0, s, 0});
+            h.put(0, 0.0, s);
+            D[s] = 0.0;
             H[s] = 0;
             R[s] = 1.0;
             P[s] = -1;
         }
         __syncthreads();
         int toReach = g.T;
-        int hsize = 1;
-        while (hsize > 0 && toReach > 0) {
-            // pop (igraph_2wheap_delete_max): the top is known before the
-            // sift-down, so its arc range and attached flag load meanwhile
-            int u = 0, hu = 0;
-            double mind = 0.0, ru = 0.0;
-            if (lane == 0) {
-                const XEnt top = reinterpret_cast<const XEnt*>(ex_smem)[0];   // hc >= 1
-                u = top.idx;
-                mind = -top.key;
-                hu = top.hops;
-                ru = top.rel;
-            }
-            u = __builtin_amdgcn_readfirstlane(u);
-            // early stop: every tied predecessor popped, parents final
-            if (tslot >= 0 && __shfl(mind, 0, 64) > thr) break;
+        int size = 1;                    // uniform
+        // SHD_PE_DEBUG_COUNTERS: cycles per pop segment (top+range, sink,
+        // arcs+pre-check, pushes), pops, pushes + modifies, heap size at exit
+        long long xc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        long long xt = xdbg ? (long long)clock64() : 0;
+        auto xtick = [&](int k) {
+            if (xdbg) { const long long t = (long long)clock64(); xc[k] += t - xt; xt = t; }
+        };
+        // early-stop rows need only the parents (k_tie_write derives hops and
+        // reliability); a relevance scan may have cleared the row (thr < 0)
+        const bool labels = tslot < 0;
+        const int ldsLevel = 30 - __builtin_clz(hc + 1);   // deepest heap level wholly in LDS
+        if (tslot >= 0 && thr < 0.0) size = 0;
+        while (size > 0 && toReach > 0) {
+            // pop (igraph_2wheap_delete_max): the vertex record of the top and
+            // the last element load together, the sink's LDS rounds overlap them
+            const int u = __builtin_amdgcn_readfirstlane(h.lidx()[0]);
+            const double mind = -h.lkey()[0];
+            if (tslot >= 0 && mind > thr) break;   // early stop: tied predecessors all popped
             const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
             const int att = g.isAttached[u];
-            if (lane == 0) {
-                const int last = h.size - 1;
-                h.size = last;
-                if (last > 0) {
-                    const XEnt e = h.load(last);
-                    h.place(h.sink_hole(0, e.key), e);
-                }
-                h.set_idx2(u, 1);
-                D[u] = mind;
-            }
-            mind = __shfl(mind, 0, 64);
-            hu = __shfl(hu, 0, 64);
-            ru = __shfl(ru, 0, 64);
+            int hu = 0;
+            double ru = 1.0;
+            if (labels) { hu = H[u]; ru = R[u]; }
+            size -= 1;
+            double km = 0.0;
+            int im = 0;
+            if (size > 0) h.get(size, km, im);       // uniform position: last element
+            if (xdbg) { asm volatile("" :: "v"(a0), "v"(a1), "v"(att)); xtick(0); xc[5]++; }
+            if (lane == 0) h.I2[u] = 1;
+            int head = 0, hl = 0;
+            bool placed = size == 0;
+            if (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
             if (att) --toReach;
-            for (int base = a0; base < a1; base += 64) {
+            // arcs in chunks of 64; the first chunk's loads and pre-check
+            // overlap the remaining sink rounds (the pre-check reads only
+            // index2 categories and tentative distances, which a sift-down
+            // does not change)
+            for (int base = a0; base < a1 || !placed; base += 64) {
                 const int a = base + lane;
                 const bool valid = a < a1;
-                const int ac = valid ? a : a0;
-                const int v = g.col[ac];
-                const double w = g.lat[ac];
-                const double rw = g.rel[ac];
-                const int ia = g.outToIn[ac];
-                if (fence) __syncthreads();   // lane 0's global heap/index2 stores visible
-                const int st = valid ? h.idx2(v) : 1;
+                int v = 0, ia = 0;
+                double w = 0.0;
+                if (valid) {
+                    v = g.col[a];
+                    w = g.lat[a];
+                    ia = g.outToIn[a];
+                }
+                if (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+                // read before the sift-down finished: categories and distances
+                // hold, heap positions may not
+                const bool posFresh = placed;
+                int st = 1;
+                double dv = 0.0;
+                if (valid) {
+                    st = h.I2[v];
+                    dv = D[v];
+                }
+                while (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+                xtick(1);
                 const double alt = mind + w;
                 int need = 0;
                 if (st == 0) need = 1;
-                else if (st >= 2) need = (alt < -h.key(st - 2)) ? 2 : 0;
-                const int nh = hu + 1;
-                const double nr = ru * rw;
-                if (need) { P[v] = ia; H[v] = nh; R[v] = nr; }
+                else if (st >= 2) need = alt < dv ? 2 : 0;
+                if (need) {
+                    P[v] = ia;
+                    D[v] = alt;
+                    if (labels) { H[v] = hu + 1; R[v] = ru * g.rel[a]; }
+                }
                 unsigned long long mask = __ballot(need != 0);
+                xtick(2);
+                if (xdbg) xc[6] += __builtin_popcountll(mask);
+                bool moved = !posFresh;    // positions read in the pre-check stale?
                 while (mask) {
                     const int k = __builtin_ctzll(mask);
                     mask &= mask - 1;
                     const int vk = __builtin_amdgcn_readlane(v, k);
                     const int nk = __builtin_amdgcn_readlane(need, k);
-                    const int hk = __builtin_amdgcn_readlane(nh, k);
                     const double ak = __shfl(alt, k, 64);
-                    const double rk = __shfl(nr, k, 64);
-                    if (lane == 0) {
-                        const XEnt e{-ak, rk, vk, hk};
-                        if (nk == 1) {            // igraph_2wheap_push_with_index
-                            const int elem = h.size;
-                            h.size = elem + 1;
-                            h.shift_up_place(elem, e);
-                        } else {                  // igraph_2wheap_modify: sink, then shift_up
-                            const int pos = h.idx2(vk) - 2;
-                            h.shift_up_place(h.sink_hole(pos, e.key), e);
-                        }
+                    if (nk == 1) {                    // igraph_2wheap_push_with_index
+                        h.shift_up(size, -ak, vk, lane);
+                        size += 1;
+                    } else {                          // igraph_2wheap_modify (sink is a no-op)
+                        const int p2 = moved ? h.I2[vk] : __builtin_amdgcn_readlane(st, k);
+                        h.shift_up(__builtin_amdgcn_readfirstlane(p2) - 2, -ak, vk, lane);
                     }
+                    moved = true;
                 }
+                xtick(3);
             }
-            hsize = __shfl(h.size, 0, 64);
-            if (fence) __syncthreads();
+        }
+        if (xdbg && lane == 0) {
+            xc[7] = size;
+            for (int k = 0; k < 8; ++k) xdbg[(size_t)b * 8 + k] = xc[k];
         }
         __syncthreads();
         if (tslot >= 0)
-            tie_finalize(tie, tslot, n, lane, [&](int v) { return h.idx2(v) != 0; }, P);
+            tie_finalize(tie, tslot, n, lane,
+                         [&](int v) { return thr >= 0.0 && h.I2[v] != 0; }, P);
         else
             write_row(g, tab, r, s,
-                      [&](int t) { return h.idx2(t) == 1 ? d2b(D[t]) : INF_BITS; },
+                      [&](int t) { return h.I2[t] == 1 ? d2b(D[t]) : INF_BITS; },
                       [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
         __syncthreads();
     }
 }
 
+// ---------------------------------------------------------------------------
 // k_exact_rows_soa: the same emulation when the whole heap and index2 fit
 // LDS (16 B per vertex: n <= 10240).  Structure-of-arrays heap (key f64,
 // idx i32) so a sift-down level reads both children's keys with one
@@ -1190,7 +1317,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
                                                                const int32_t* __restrict__ rows,
                                                                int32_t nRows,
                                                                const int32_t* __restrict__ slots,
-                                                               TieBuf tie) {
+                                                               TieBuf tie, long long* xdbg) {
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
@@ -1250,7 +1377,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
         const int s = g.attached[r];
         const int tslot = slots ? slots[b] : -1;
         const double thr = tslot >= 0 ? tie.thr[tslot] : 0.0;
-        for (int v = lane; v < n; v += EX_THREADS) index2[v] = 0;
+        for (int v = lane; v < n; v += EX_THREADS) index2[v] = 0;   // (LDS: cheap)
         if (lane == 0) {
             place(0, 0.0, s);
             H[s] = 0;
@@ -1258,7 +1385,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
             P[s] = -1;
         }
         __syncthreads();
-        int size = 1;                     // uniform (every lane tracks it)
+        int size = tslot >= 0 && thr < 0.0 ? 0 : 1;   // uniform; 0: relevance scan cleared the row
         int toReach = g.T;
         while (size > 0 && toReach > 0) {
             // pop: top known before the sift-down, its arc range loads meanwhile
@@ -1322,7 +1449,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
         }
         __syncthreads();
         if (tslot >= 0)
-            tie_finalize(tie, tslot, n, lane, [&](int v) { return index2[v] != 0; }, P);
+            tie_finalize(tie, tslot, n, lane, [&](int v) { return thr >= 0.0 && index2[v] != 0; }, P);
         else
             write_row(g, tab, r, s,
                       [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
@@ -1422,6 +1549,13 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
         launch_sparse_layout<0>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
 }
 
+void launch_tie_scan(const DevGraph& g, const int32_t* dRows, const int32_t* dSlots,
+                     int32_t nRows, const TieBuf& tie, void* stream) {
+    if (nRows <= 0) return;
+    hipLaunchKernelGGL(k_tie_scan, dim3(nRows), dim3(1024), 0,
+                       reinterpret_cast<hipStream_t>(stream), g, dRows, dSlots, tie);
+}
+
 void launch_tie_write(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
                       const int32_t* dSlots, int32_t nRows, const TieBuf& tie, void* stream) {
     if (nRows <= 0) return;
@@ -1429,10 +1563,12 @@ void launch_tie_write(const DevGraph& g, const DevTable& tab, const int32_t* dRo
                        reinterpret_cast<hipStream_t>(stream), g, tab, dRows, dSlots, tie);
 }
 
+int exact_soa_max_n() { return EX_SOA_MAXN; }
+
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
-                       bool ldsIndex, bool forceGlobalHeap, const int32_t* dSlots,
-                       const TieBuf& tie, void* stream) {
+                       bool forceGlobalHeap, const int32_t* dSlots, const TieBuf& tie,
+                       long long* dXdbg, void* stream) {
     if (nRows <= 0) return;
     if (grid > nRows) grid = nRows;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1441,21 +1577,14 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows_soa),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, sb);
         hipLaunchKernelGGL(k_exact_rows_soa, dim3(grid), dim3(EX_THREADS), sb, st, g, tab, sc,
-                           dRows, nRows, dSlots, tie);
+                           dRows, nRows, dSlots, tie, dXdbg);
         return;
     }
-    const int bytes = (int)(((size_t)24 * hc + (ldsIndex ? (size_t)4 * g.n : 0) + 15) & ~(size_t)15);
-    if (ldsIndex) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-        hipLaunchKernelGGL(k_exact_rows<true>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab,
-                           sc, dRows, nRows, hc, dSlots, tie);
-    } else {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-        hipLaunchKernelGGL(k_exact_rows<false>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab,
-                           sc, dRows, nRows, hc, dSlots, tie);
-    }
+    const int bytes = (int)(((size_t)12 * hc + 15) & ~(size_t)15);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    hipLaunchKernelGGL(k_exact_rows, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc, dRows,
+                       nRows, hc, dSlots, tie, dXdbg);
 }
 
 void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,

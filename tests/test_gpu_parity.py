@@ -424,3 +424,13 @@ def test_batched_tie_rows_early_stop(E, oracle_mod, k, vloss, directed):
     assert st["rowsTieEarly"] > 0
     if 2 * k > 254:
         assert st["rowsTieEarly"] < st["rowsExact"]
+
+
+def test_batched_tie_rows_partial_targets(E, oracle_mod):
+    """Quantised latencies with 1 of 5 vertices attached: ambiguous entries
+    off every target's path are cleared by the relevance scan (fast-path
+    parents kept), the rest run the early-stop emulation."""
+    top = G.random_sparse(3000, 5, seed=77, quantum=1.0)
+    att = np.arange(0, 3000, 5, dtype=np.int32)
+    st = _check_engine(E, oracle_mod, top, att, force=5)
+    assert st["mode"] == 1 and st["rowsTieEarly"] > 0
