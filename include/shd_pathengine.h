@@ -63,6 +63,7 @@ extern "C" {
 #define SHD_PE_F_EXACT       0x10u /* row had equal-distance predecessor ties and
                                       was resolved by the on-GPU igraph-heap kernel */
 #define SHD_PE_F_FAILED (SHD_PE_F_UNREACHABLE | SHD_PE_F_NOEDGE)
+#define SHD_PE_F_INVALID     0x80u /* batched helpers: vertex id out of range      */
 
 /* ---- graph description (built once by host C from igraph) ------------- */
 /* Edges in igraph edge-id order (GraphML document order), endpoints as
@@ -231,6 +232,30 @@ int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbp
 
 int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out);
 int shd_pe_reset_stats(ShdPe* pe);
+
+/* ---- batched helpers on the device ------------
+ * The per-query lookups below, for many queries in one call: inputs and
+ * outputs are host arrays of `count` entries (staged through the engine's
+ * device in chunks).  Results are bit-identical to the one-query helpers. */
+
+/* _topology_computeShortestPathToSelf (topology.c:1545-1653) per vertex:
+ * lat = 2 * w_min, rel = (1 - loss_min)^2 over v's OUT-incident edges (the
+ * first strict minimum in igraph incidence order).  flags[i]:
+ * 0, SHD_PE_F_NOEDGE (graph has no edges), SHD_PE_F_INVALID (bad id). */
+int shd_pe_self_paths(ShdPe* pe, const int32_t* vertices, int32_t count, double* lat,
+                      double* rel, uint8_t* flags);
+/* _topology_lookupDirectPath (topology.c:1877-1927) per pair (src[i],dst[i]):
+ * flags[i] = SHD_PE_F_DIRECT with lat/rel, SHD_PE_F_NOEDGE (lat = rel = 0),
+ * or SHD_PE_F_INVALID. */
+int shd_pe_direct_paths(ShdPe* pe, const int32_t* src, const int32_t* dst, int64_t count,
+                        double* lat, double* rel, uint8_t* flags);
+/* _topology_verticesAreAdjacent (topology.c:1248-1264) per pair: out[i] 1 / 0
+ * (0 for an invalid id; s == t is adjacent iff s has a self-loop). */
+int shd_pe_adjacent_pairs(ShdPe* pe, const int32_t* src, const int32_t* dst, int64_t count,
+                          uint8_t* out);
+/* _topology_isComplete (topology.c:450-552) evaluated on the device from the
+ * resident CSR: *isComplete = 1 / 0 (agrees with shd_pe_is_complete). */
+int shd_pe_is_complete_device(ShdPe* pe, int32_t* isComplete);
 
 /* ---- host-side helpers Shadow keeps in C (no GPU work) ----------------- */
 /* _topology_lookupDirectPath (topology.c:1877-1927) for one pair. */

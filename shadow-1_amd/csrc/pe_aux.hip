@@ -1,0 +1,170 @@
+// pe_aux.hip -- batched per-vertex / per-pair helpers of the path table
+// (SURVEY.md §8(f) rank 3): the lookups Shadow otherwise does one at a time
+// on the host, with igraph attribute calls per query.
+//
+//   k_self_paths    _topology_computeShortestPathToSelf  topology.c:1545-1653
+//   k_pairs         _topology_lookupDirectPath           topology.c:1877-1927
+//                   _topology_verticesAreAdjacent        topology.c:1248-1264
+//   k_incident_min  _topology_isComplete                 topology.c:450-552
+//
+// All are gathers over the CSR (col / lat / rel, rows sorted by neighbour id
+// = igraph incidence order): HBM/L2 latency-bound, no arithmetic to speak of.
+#include <hip/hip_runtime.h>
+
+#include "pe_device.hpp"
+#include "pe_devutil.hpp"
+
+namespace shdpe {
+
+// first arc of row s with col >= t (igraph_get_eid on a sorted incidence row)
+__device__ __forceinline__ int row_lower_bound(const DevGraph& g, int s, int t) {
+    int lo = g.rowPtr[s], hi = g.rowPtr[s + 1];
+    while (lo < hi) {
+        const int mid = lo + ((hi - lo) >> 1);
+        if (g.col[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// One wave per vertex.  The reference walks v's OUT-incident edges in igraph
+// order (ascending neighbour, the self-loop in place) and keeps the first
+// strict minimum of the latency (the minLatency == 0 sentinel of :1592 only
+// seeds it: latencies are > 0).  That is the lexicographic minimum of
+// (latency, incidence position): lanes take strided arcs, then a wave
+// reduction.  lat = 2 * w_min, rel = r_min * r_min (:1640-1641).
+__global__ __launch_bounds__(256) void k_self_paths(DevGraph g0, const int32_t* __restrict__ verts,
+                                                    int32_t count, int64_t nEdges,
+                                                    double* __restrict__ lat,
+                                                    double* __restrict__ rel,
+                                                    uint8_t* __restrict__ flags) {
+    const DevGraph g = global_view(g0);
+    const int w = (int)(((size_t)blockIdx.x * 256 + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= count) return;                                   // uniform per wave
+    const int v = verts[w];
+    if (v < 0 || v >= g.n) {
+        if (lane == 0) { lat[w] = 0.0; rel[w] = 0.0; flags[w] = F_INVALID; }
+        return;
+    }
+    const int b = g.rowPtr[v], e = g.rowPtr[v + 1];
+    const int sp = row_lower_bound(g, v, v) - b;               // self-loop's incidence slot
+    const bool self = g.hasSelf[v] != 0;
+    double bl = INFINITY, br = 0.0;
+    int bp = INT32_MAX;
+    for (int a = b + lane; a < e; a += 64) {
+        const double L = g.lat[a];
+        const int pos = (a - b) + ((self && a - b >= sp) ? 1 : 0);
+        if (L < bl || (L == bl && pos < bp)) { bl = L; bp = pos; br = g.rel[a]; }
+    }
+    if (lane == 0 && self) {
+        const double L = g.selfLat[v];
+        if (L < bl || (L == bl && sp < bp)) { bl = L; bp = sp; br = g.selfRel[v]; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ol = __shfl_xor(bl, o, 64);
+        const double orr = __shfl_xor(br, o, 64);
+        const int op = __shfl_xor(bp, o, 64);
+        if (ol < bl || (ol == bl && op < bp)) { bl = ol; bp = op; br = orr; }
+    }
+    if (lane == 0) {
+        if (bp == INT32_MAX) {
+            // no incident edge: minLatency stays 0 (lat 0, rel 0); the
+            // reference errors out only on an edgeless graph
+            lat[w] = 0.0;
+            rel[w] = 0.0;
+            flags[w] = nEdges == 0 ? F_NOEDGE : 0;
+        } else {
+            lat[w] = 2.0 * bl;
+            rel[w] = br * br;
+            flags[w] = 0;
+        }
+    }
+}
+
+// One thread per pair.  mode 0: direct path (lat = 0.0 + w, rel =
+// ((1 * a_s) * a_t) * r_e, flags F_DIRECT or F_NOEDGE); mode 1: adjacency
+// only (flags[i] = 1 adjacent, 0 not; s == t adjacent iff it has a loop).
+__global__ __launch_bounds__(256) void k_pairs(DevGraph g0, const int32_t* __restrict__ src,
+                                               const int32_t* __restrict__ dst, int64_t count,
+                                               int mode, double* __restrict__ lat,
+                                               double* __restrict__ rel,
+                                               uint8_t* __restrict__ flags) {
+    const DevGraph g = global_view(g0);
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const int s = src[i], t = dst[i];
+    if (s < 0 || s >= g.n || t < 0 || t >= g.n) {
+        if (mode == 0) { lat[i] = 0.0; rel[i] = 0.0; }
+        flags[i] = mode == 0 ? F_INVALID : 0;
+        return;
+    }
+    int a = -1;
+    bool found;
+    if (s == t) {
+        found = g.hasSelf[s] != 0;
+    } else {
+        a = row_lower_bound(g, s, t);
+        found = a < g.rowPtr[s + 1] && g.col[a] == t;
+    }
+    if (mode == 1) {
+        flags[i] = found ? 1 : 0;
+        return;
+    }
+    double acc = 1.0 * g.vrel[s];                            // :1901-1907
+    acc = acc * g.vrel[t];
+    double L = 0.0, R = 0.0;
+    uint8_t f = F_NOEDGE;
+    if (found) {
+        const double w = s == t ? g.selfLat[s] : g.lat[a];
+        const double r = s == t ? g.selfRel[s] : g.rel[a];
+        L = 0.0 + w;                                          // :1920
+        R = acc * r;                                          // :1921
+        f = F_DIRECT;
+    }
+    lat[i] = L;
+    rel[i] = R;
+    flags[i] = f;
+}
+
+// _topology_isComplete: every vertex's incident count (self-loop counted
+// twice undirected, then corrected by one) must reach n.  Minimum count.
+__global__ __launch_bounds__(256) void k_incident_min(DevGraph g0, int32_t* out) {
+    const DevGraph g = global_view(g0);
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    int c = INT32_MAX;
+    if (v < g.n) {
+        c = g.rowPtr[v + 1] - g.rowPtr[v];
+        // a loop counts once directed; twice undirected, minus the one
+        // correction of :505-519 -- once either way
+        if (g.hasSelf[v]) c += 1;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c = min(c, __shfl_xor(c, o, 64));
+    if ((threadIdx.x & 63) == 0 && c != INT32_MAX) atomicMin(out, c);
+}
+
+void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, int64_t nEdges,
+                       double* dLat, double* dRel, uint8_t* dFlags, void* stream) {
+    if (count <= 0) return;
+    const int blocks = (int)(((int64_t)count * 64 + 255) / 256);
+    hipLaunchKernelGGL(k_self_paths, dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), g, dVerts, count, nEdges, dLat,
+                       dRel, dFlags);
+}
+
+void launch_pairs(const DevGraph& g, const int32_t* dSrc, const int32_t* dDst, int64_t count,
+                  int mode, double* dLat, double* dRel, uint8_t* dFlags, void* stream) {
+    if (count <= 0) return;
+    hipLaunchKernelGGL(k_pairs, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), g, dSrc, dDst, count, mode, dLat,
+                       dRel, dFlags);
+}
+
+void launch_incident_min(const DevGraph& g, int32_t* dOut, void* stream) {
+    hipLaunchKernelGGL(k_incident_min, dim3((g.n + 255) / 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), g, dOut);
+}
+
+}  // namespace shdpe

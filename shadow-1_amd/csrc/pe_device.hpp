@@ -138,6 +138,7 @@ constexpr uint8_t F_NOEDGE = 0x02;
 constexpr uint8_t F_ZEROLAT = 0x04;
 constexpr uint8_t F_DIRECT = 0x08;
 constexpr uint8_t F_EXACT = 0x10;
+constexpr uint8_t F_INVALID = 0x80;   // batched helpers: vertex id out of range
 
 struct SparseLaunch {
     int32_t threads;     // workgroup size
@@ -187,6 +188,13 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
                        const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream);
 const void* batch_kernel_ptr(int lb);
 int batch_lds_bytes(int n);
+// batched helpers (pe_aux.hip), all on `stream`
+void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, int64_t nEdges,
+                       double* dLat, double* dRel, uint8_t* dFlags, void* stream);
+// mode 0 direct paths (lat, rel, flags), mode 1 adjacency (flags = 0 / 1)
+void launch_pairs(const DevGraph& g, const int32_t* dSrc, const int32_t* dDst, int64_t count,
+                  int mode, double* dLat, double* dRel, uint8_t* dFlags, void* stream);
+void launch_incident_min(const DevGraph& g, int32_t* dOut, void* stream);
 // dense path (pe_dense.hip)
 void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int64_t nArcs,
                         void* stream);

@@ -1497,6 +1497,101 @@ extern "C" int shd_pe_adjacent(const ShdPe* pe, int32_t s, int32_t t) {
     return pe->hg.findArc(s, t) != -1 ? 1 : 0;
 }
 
+// ---- batched helpers (pe_aux.hip) ----------------------------------------
+// Inputs / outputs are host arrays; chunks of up to 16M entries are staged
+// through device buffers owned by the call, on shard 0's device and stream.
+namespace {
+struct AuxBufs {
+    void* p[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    ~AuxBufs() { for (void* x : p) if (x) (void)hipFree(x); }
+};
+constexpr int64_t AUX_CHUNK = (int64_t)1 << 24;
+}  // namespace
+
+extern "C" int shd_pe_self_paths(ShdPe* pe, const int32_t* vertices, int32_t count, double* lat,
+                                 double* rel, uint8_t* flags) {
+    if (!pe || count < 0 || (count > 0 && (!vertices || !lat || !rel || !flags))) return SHD_PE_EINVAL;
+    if (count == 0) return SHD_PE_OK;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    Shard* sh = pe->shards[0].get();
+    HIPCHK(hipSetDevice(sh->device));
+    const int64_t ch = std::min<int64_t>(count, AUX_CHUNK);
+    AuxBufs b;
+    if (hipMalloc(&b.p[0], ch * 4) || hipMalloc(&b.p[1], ch * 8) || hipMalloc(&b.p[2], ch * 8) ||
+        hipMalloc(&b.p[3], ch))
+        return SHD_PE_ENOMEM;
+    for (int64_t c0 = 0; c0 < count; c0 += ch) {
+        const int32_t c = (int32_t)std::min<int64_t>(ch, count - c0);
+        HIPCHK(hipMemcpyAsync(b.p[0], vertices + c0, (size_t)c * 4, hipMemcpyHostToDevice, sh->stream));
+        launch_self_paths(sh->dg, (const int32_t*)b.p[0], c, pe->hg.nEdges, (double*)b.p[1],
+                          (double*)b.p[2], (uint8_t*)b.p[3], sh->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(lat + c0, b.p[1], (size_t)c * 8, hipMemcpyDeviceToHost, sh->stream));
+        HIPCHK(hipMemcpyAsync(rel + c0, b.p[2], (size_t)c * 8, hipMemcpyDeviceToHost, sh->stream));
+        HIPCHK(hipMemcpyAsync(flags + c0, b.p[3], (size_t)c, hipMemcpyDeviceToHost, sh->stream));
+        HIPCHK(hipStreamSynchronize(sh->stream));
+    }
+    return SHD_PE_OK;
+}
+
+static int pairs_call(ShdPe* pe, const int32_t* src, const int32_t* dst, int64_t count, int mode,
+                      double* lat, double* rel, uint8_t* flags) {
+    if (!pe || count < 0 || (count > 0 && (!src || !dst || !flags || (mode == 0 && (!lat || !rel)))))
+        return SHD_PE_EINVAL;
+    if (count == 0) return SHD_PE_OK;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    Shard* sh = pe->shards[0].get();
+    HIPCHK(hipSetDevice(sh->device));
+    const int64_t ch = std::min<int64_t>(count, AUX_CHUNK);
+    AuxBufs b;
+    if (hipMalloc(&b.p[0], ch * 4) || hipMalloc(&b.p[1], ch * 4) || hipMalloc(&b.p[4], ch) ||
+        (mode == 0 && (hipMalloc(&b.p[2], ch * 8) || hipMalloc(&b.p[3], ch * 8))))
+        return SHD_PE_ENOMEM;
+    for (int64_t c0 = 0; c0 < count; c0 += ch) {
+        const int64_t c = std::min<int64_t>(ch, count - c0);
+        HIPCHK(hipMemcpyAsync(b.p[0], src + c0, (size_t)c * 4, hipMemcpyHostToDevice, sh->stream));
+        HIPCHK(hipMemcpyAsync(b.p[1], dst + c0, (size_t)c * 4, hipMemcpyHostToDevice, sh->stream));
+        launch_pairs(sh->dg, (const int32_t*)b.p[0], (const int32_t*)b.p[1], c, mode,
+                     (double*)b.p[2], (double*)b.p[3], (uint8_t*)b.p[4], sh->stream);
+        HIPCHK(hipGetLastError());
+        if (mode == 0) {
+            HIPCHK(hipMemcpyAsync(lat + c0, b.p[2], (size_t)c * 8, hipMemcpyDeviceToHost, sh->stream));
+            HIPCHK(hipMemcpyAsync(rel + c0, b.p[3], (size_t)c * 8, hipMemcpyDeviceToHost, sh->stream));
+        }
+        HIPCHK(hipMemcpyAsync(flags + c0, b.p[4], (size_t)c, hipMemcpyDeviceToHost, sh->stream));
+        HIPCHK(hipStreamSynchronize(sh->stream));
+    }
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_pe_direct_paths(ShdPe* pe, const int32_t* src, const int32_t* dst, int64_t count,
+                                   double* lat, double* rel, uint8_t* flags) {
+    return pairs_call(pe, src, dst, count, 0, lat, rel, flags);
+}
+
+extern "C" int shd_pe_adjacent_pairs(ShdPe* pe, const int32_t* src, const int32_t* dst,
+                                     int64_t count, uint8_t* out) {
+    return pairs_call(pe, src, dst, count, 1, nullptr, nullptr, out);
+}
+
+extern "C" int shd_pe_is_complete_device(ShdPe* pe, int32_t* isComplete) {
+    if (!pe || !isComplete) return SHD_PE_EINVAL;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    Shard* sh = pe->shards[0].get();
+    HIPCHK(hipSetDevice(sh->device));
+    AuxBufs b;
+    if (hipMalloc(&b.p[0], 4)) return SHD_PE_ENOMEM;
+    const int32_t init = INT32_MAX;
+    HIPCHK(hipMemcpyAsync(b.p[0], &init, 4, hipMemcpyHostToDevice, sh->stream));
+    launch_incident_min(sh->dg, (int32_t*)b.p[0], sh->stream);
+    HIPCHK(hipGetLastError());
+    int32_t mn = 0;
+    HIPCHK(hipMemcpyAsync(&mn, b.p[0], 4, hipMemcpyDeviceToHost, sh->stream));
+    HIPCHK(hipStreamSynchronize(sh->stream));
+    *isComplete = mn >= pe->hg.n ? 1 : 0;
+    return SHD_PE_OK;
+}
+
 // exported for the host topology mirror (pe_topology.cpp)
 const shdpe::HostGraph* shd_pe_host_graph(const ShdPe* pe) { return pe ? &pe->hg : nullptr; }
 int32_t shd_pe_position(const ShdPe* pe, int32_t v) {

@@ -21,6 +21,7 @@ ENOTOWNED, ETOOBIG, ECOMM = -10, -11, -12
 DEBUG_ENV, DEBUG_COUNTERS = 0x1, 0x2
 F_UNREACHABLE, F_NOEDGE, F_ZEROLAT, F_DIRECT, F_EXACT = 0x01, 0x02, 0x04, 0x08, 0x10
 F_FAILED = F_UNREACHABLE | F_NOEDGE
+F_INVALID = 0x80
 
 EXPORTS = [
     "shd_pe_default_options", "shd_pe_create", "shd_pe_destroy", "shd_pe_strerror",
@@ -29,7 +30,8 @@ EXPORTS = [
     "shd_pe_copy_rows_device", "shd_pe_synchronize", "shd_pe_get_stats", "shd_pe_reset_stats",
     "shd_pe_stream_bandwidth", "shd_pe_num_shards", "shd_pe_shard_bounds", "shd_pe_plan_shards", "shd_pe_owned_range",
     "shd_pe_gather", "shd_pe_comm_unique_id", "shd_pe_comm_init",
-    "shd_pe_direct_path", "shd_pe_self_path", "shd_pe_adjacent", "shd_topology_new",
+    "shd_pe_direct_path", "shd_pe_self_path", "shd_pe_adjacent", "shd_pe_self_paths",
+    "shd_pe_direct_paths", "shd_pe_adjacent_pairs", "shd_pe_is_complete_device", "shd_topology_new",
     "shd_topology_free", "shd_topology_get_latency", "shd_topology_get_reliability",
     "shd_topology_is_routable", "shd_topology_increment_path_packet_counter",
     "shd_topology_cached", "shd_topology_min_latency", "shd_topology_cache_size",
@@ -112,6 +114,10 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_direct_path": (C.c_int, [vp, i32, i32, vp, vp]),
         "shd_pe_self_path": (C.c_int, [vp, i32, vp, vp]),
         "shd_pe_adjacent": (C.c_int, [vp, i32, i32]),
+        "shd_pe_self_paths": (C.c_int, [vp, vp, i32, vp, vp, vp]),
+        "shd_pe_direct_paths": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
+        "shd_pe_adjacent_pairs": (C.c_int, [vp, vp, vp, i64, vp]),
+        "shd_pe_is_complete_device": (C.c_int, [vp, vp]),
         "shd_topology_new": (C.c_int, [vp, i32, vp]),
         "shd_topology_free": (None, [vp]),
         "shd_topology_get_latency": (f64, [vp, i32, i32]),
@@ -287,6 +293,42 @@ class Engine:
         lat, rel = C.c_double(), C.c_double()
         rc = self._lib.shd_pe_self_path(self.h, int(v), C.byref(lat), C.byref(rel))
         return None if rc else (lat.value, rel.value)
+
+    # ---- batched helpers on the device (pe_aux.hip) ----
+    def self_paths(self, vertices):
+        v = np.ascontiguousarray(vertices, dtype=np.int32)
+        n = v.shape[0]
+        lat, rel, flags = np.empty(n), np.empty(n), np.empty(n, np.uint8)
+        self._chk(self._lib.shd_pe_self_paths(self.h, _p(v), n, _p(lat), _p(rel), _p(flags)),
+                  "shd_pe_self_paths")
+        return lat, rel, flags
+
+    def direct_paths(self, src, dst):
+        s = np.ascontiguousarray(src, dtype=np.int32)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        if s.shape != d.shape:
+            raise ValueError("src/dst shapes differ")
+        n = s.shape[0]
+        lat, rel, flags = np.empty(n), np.empty(n), np.empty(n, np.uint8)
+        self._chk(self._lib.shd_pe_direct_paths(self.h, _p(s), _p(d), n, _p(lat), _p(rel),
+                                                _p(flags)), "shd_pe_direct_paths")
+        return lat, rel, flags
+
+    def adjacent_pairs(self, src, dst):
+        s = np.ascontiguousarray(src, dtype=np.int32)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        if s.shape != d.shape:
+            raise ValueError("src/dst shapes differ")
+        out = np.empty(s.shape[0], np.uint8)
+        self._chk(self._lib.shd_pe_adjacent_pairs(self.h, _p(s), _p(d), s.shape[0], _p(out)),
+                  "shd_pe_adjacent_pairs")
+        return out
+
+    def is_complete_device(self) -> bool:
+        x = C.c_int32(0)
+        self._chk(self._lib.shd_pe_is_complete_device(self.h, C.byref(x)),
+                  "shd_pe_is_complete_device")
+        return bool(x.value)
 
 
 class TopologyShim:
