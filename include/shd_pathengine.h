@@ -266,6 +266,45 @@ int shd_pe_self_path(const ShdPe* pe, int32_t v, double* lat, double* rel);
 int shd_pe_adjacent(const ShdPe* pe, int32_t s, int32_t t);
 
 /* ------------------------------------------------------------------------
+ * Path cache as a dense triangular row store,
+ * replacing topology.c's GHashTable<src, GHashTable<dst, Path*>>
+ * (_topology_getPathFromCache :1284-1305, _topology_shouldStorePath
+ * :1307-1336, _topology_storePathInCache :1338-1386, Path path.c:13-38).
+ * Keys are vertex indices of attached vertices; one 25-B slot per unordered
+ * pair (the store rule never keeps both directions), remembering the
+ * direction it was stored under.  Thread safety: get / increment never lock
+ * and may run concurrently with each other and with stores; stores
+ * serialise internally.  No GPU work; usable without an engine.
+ * ---------------------------------------------------------------------- */
+typedef struct ShdRowStore ShdRowStore;
+
+int shd_rowstore_new(int32_t nVertices, const int32_t* attached, int32_t nAttached,
+                     ShdRowStore** out);
+void shd_rowstore_free(ShdRowStore* st);
+/* _topology_getPathFromCache(s, d): 1 and the Path fields if an entry was
+ * stored under exactly (s, d), else 0. */
+int shd_rowstore_get(const ShdRowStore* st, int32_t s, int32_t d, double* lat, double* rel,
+                     int32_t* isDirect, uint64_t* packetCount);
+/* _topology_storePathInCache: 1 stored, 0 refused by _topology_shouldStorePath
+ * (either direction cached; a non-direct path on a complete graph; a
+ * non-direct path for an adjacent pair under prefersDirectPaths -- the caller
+ * passes isComplete and preferDirectAndAdjacent), < 0 error. */
+int shd_rowstore_store(ShdRowStore* st, int32_t s, int32_t d, int32_t isDirect,
+                       int32_t isComplete, int32_t preferDirectAndAdjacent, double lat,
+                       double rel);
+/* One engine row of source s (T entries in attached order, as shd_pe_get_row
+ * returns them) through the per-target loop of topology.c:1815-1859.
+ * adjacent (optional): adjacent[j] = prefersDirectPaths && (s, attached[j])
+ * is an edge.  Returns 1 if every target succeeded, 0 if not, < 0 error. */
+int shd_rowstore_store_row(ShdRowStore* st, int32_t s, const double* lat, const double* rel,
+                           const uint8_t* flags, int32_t isComplete, const uint8_t* adjacent);
+/* topology_incrementPathPacketCounter on a cached entry: 0, or -1 if absent. */
+int shd_rowstore_increment(ShdRowStore* st, int32_t s, int32_t d);
+int64_t shd_rowstore_size(const ShdRowStore* st);
+double shd_rowstore_min_latency(const ShdRowStore* st);
+int64_t shd_rowstore_memory_bytes(const ShdRowStore* st);
+
+/* ------------------------------------------------------------------------
  * Host mirror of the topology.c path API (the drop-in seen by worker.c,
  * tcp.c, host.c): _topology_getPathEntry + the two-level path cache, with
  * rows coming from the engine.  Queries are by vertex index; Shadow's

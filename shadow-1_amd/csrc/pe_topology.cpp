@@ -15,6 +15,7 @@
 // value depends on query order (self path vs. self-loop row entry), and a
 // row with any failed target makes the triggering lookup fail even if its
 // own entry was stored.
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -28,70 +29,42 @@
 const shdpe::HostGraph* shd_pe_host_graph(const ShdPe* pe);
 int32_t shd_pe_position(const ShdPe* pe, int32_t v);
 
-// Dense host row store, replacing the reference's
-// two-level GHashTable<src, GHashTable<dst, Path*>> (topology.c:1284-1386,
-// path.c:13-38): one row per attached SOURCE ordinal, allocated on its first
-// insert, with a state byte per attached DESTINATION ordinal (0 absent,
-// 1 stored, 2 stored + isDirect) and the Path fields side by side.  Lookups
-// and the should-store test are two array reads instead of two hash probes
-// under rwlocks; a row insert is a sequential pass.  Semantics are the
-// reference's, entry for entry.
-namespace {
-struct PathRow {
-    std::vector<double> lat, rel;
-    std::vector<int64_t> packets;
-    std::vector<uint8_t> state;
-    explicit PathRow(size_t T) : lat(T), rel(T), packets(T, 0), state(T, 0) {}
-};
-struct PathRef {                    // a cached Path: row + destination ordinal
-    PathRow* row = nullptr;
-    int32_t j = -1;
-    explicit operator bool() const { return row != nullptr; }
-};
-}  // namespace
-
+// The path cache is the triangular row store of pe_rowstore.cpp (SURVEY.md
+// §8f rank 1; topology.c:1284-1386).  Cache hits never lock (the reference
+// takes a reader lock per probe); a miss takes the topology mutex, probes
+// again and computes -- the reference serialises the same work on
+// graphLock / the cache writer lock.
 struct ShdTopology {
     ShdPe* pe = nullptr;
     const shdpe::HostGraph* g = nullptr;
     int32_t prefersDirectPaths = 0;
-    std::vector<std::unique_ptr<PathRow>> rows;   // by attached ordinal of the source
-    int64_t cacheSize = 0;
-    double minimumPathLatency = 0.0;
-    int64_t rowsComputed = 0;
+    ShdRowStore* store = nullptr;
+    std::atomic<int64_t> rowsComputed{0};
     bool allComputed = false;
     std::vector<double> rlat, rrel;
-    std::vector<uint8_t> rflags;
+    std::vector<uint8_t> rflags, radj;
     std::vector<int32_t> attached;
-    std::mutex mu;
+    std::mutex mu;                      // misses: row computation + inserts
+    ~ShdTopology() { shd_rowstore_free(store); }
 };
 
-static PathRef cache_get(const ShdTopology* t, int32_t s, int32_t d) {
-    const int32_t ps = shd_pe_position(t->pe, s), pd = shd_pe_position(t->pe, d);
-    if (ps < 0 || pd < 0) return PathRef{};
-    PathRow* r = t->rows[ps].get();
-    if (!r || !r->state[pd]) return PathRef{};
-    return PathRef{r, pd};
-}
+namespace {
+struct PathVal {
+    bool ok = false;
+    double lat = 0.0, rel = 0.0;
+};
+}  // namespace
 
-static bool should_store(ShdTopology* t, bool isDirect, int32_t s, int32_t d) {
-    if (cache_get(t, s, d) || cache_get(t, d, s)) return false;
-    if (t->g->isComplete && !isDirect) return false;
-    if (t->prefersDirectPaths && !isDirect && t->g->findArc(s, d) != -1) return false;
-    return true;
+static bool cache_has(const ShdTopology* t, int32_t s, int32_t d, PathVal* v) {
+    return shd_rowstore_get(t->store, s, d, v ? &v->lat : nullptr, v ? &v->rel : nullptr,
+                            nullptr, nullptr) == 1;
 }
 
 static void store_path(ShdTopology* t, bool isDirect, int32_t s, int32_t d, double lat,
                        double rel) {
-    if (!should_store(t, isDirect, s, d)) return;
-    const int32_t ps = shd_pe_position(t->pe, s), pd = shd_pe_position(t->pe, d);
-    auto& row = t->rows[ps];
-    if (!row) row.reset(new PathRow(t->attached.size()));
-    row->lat[pd] = lat;
-    row->rel[pd] = rel;
-    row->packets[pd] = 0;
-    row->state[pd] = isDirect ? 2 : 1;
-    t->cacheSize++;
-    if (t->minimumPathLatency == 0 || lat < t->minimumPathLatency) t->minimumPathLatency = lat;
+    const int adjacentPref = t->prefersDirectPaths && !isDirect && t->g->findArc(s, d) != -1;
+    (void)shd_rowstore_store(t->store, s, d, isDirect ? 1 : 0, t->g->isComplete ? 1 : 0,
+                             adjacentPref, lat, rel);
 }
 
 static bool compute_source_paths(ShdTopology* t, int32_t s, int32_t d) {
@@ -110,40 +83,45 @@ static bool compute_source_paths(ShdTopology* t, int32_t s, int32_t d) {
     if (shd_pe_get_row(t->pe, s, t->rlat.data(), t->rrel.data(), nullptr, nullptr,
                        t->rflags.data()))
         return false;
-    t->rowsComputed++;
+    t->rowsComputed.fetch_add(1, std::memory_order_relaxed);
+    const uint8_t* adj = nullptr;
+    if (t->prefersDirectPaths) {
+        for (size_t j = 0; j < T; ++j) t->radj[j] = t->g->findArc(s, t->attached[j]) != -1;
+        adj = t->radj.data();
+    }
     // topology.c:1815-1859: an empty igraph path (unreachable target) is
     // skipped WITHOUT clearing isAllSuccess; only a failed fold
     // (_topology_computePathProperties, e.g. a missing (s,s) self-loop) does
-    bool allSuccess = true;
-    for (size_t j = 0; j < T; ++j) {
-        if (t->rflags[j] & SHD_PE_F_UNREACHABLE) continue;
-        if (t->rflags[j] & SHD_PE_F_NOEDGE) { allSuccess = false; continue; }
-        store_path(t, false, s, t->attached[j], t->rlat[j], t->rrel[j]);
-    }
-    return allSuccess;
+    return shd_rowstore_store_row(t->store, s, t->rlat.data(), t->rrel.data(), t->rflags.data(),
+                                  t->g->isComplete ? 1 : 0, adj) == 1;
 }
 
-static PathRef get_path_entry(ShdTopology* t, int32_t s, int32_t d) {
+// _topology_getPathEntry (topology.c:1969-2051): (s,d), then (d,s) when
+// undirected; a miss computes (direct path or source row) and re-reads both.
+static PathVal get_path_entry(ShdTopology* t, int32_t s, int32_t d, int32_t* hitS,
+                              int32_t* hitD) {
     const shdpe::HostGraph* g = t->g;
-    if (s < 0 || s >= g->n || d < 0 || d >= g->n) return PathRef{};
-    if (shd_pe_position(t->pe, s) < 0 || shd_pe_position(t->pe, d) < 0) return PathRef{};
-    PathRef p = cache_get(t, s, d);
-    if (!p && !g->directed) p = cache_get(t, d, s);
-    if (!p) {
-        bool success;
-        const bool adjacent = g->findArc(s, d) != -1;
-        if (g->isComplete || (t->prefersDirectPaths && adjacent)) {
-            double lat, rel;
-            success = shdpe::host_direct_path(*g, s, d, &lat, &rel) == SHD_PE_OK;
-            if (success) store_path(t, true, s, d, lat, rel);
-        } else {
-            success = compute_source_paths(t, s, d);
-        }
-        if (success) {
-            p = cache_get(t, s, d);
-            if (!p) p = cache_get(t, d, s);
-        }
+    PathVal p;
+    if (s < 0 || s >= g->n || d < 0 || d >= g->n) return p;
+    if (shd_pe_position(t->pe, s) < 0 || shd_pe_position(t->pe, d) < 0) return p;
+    auto probe = [&](bool afterMiss) {
+        if (cache_has(t, s, d, &p)) { *hitS = s; *hitD = d; return true; }
+        if ((afterMiss || !g->directed) && cache_has(t, d, s, &p)) { *hitS = d; *hitD = s; return true; }
+        return false;
+    };
+    if (probe(false)) { p.ok = true; return p; }
+    std::lock_guard<std::mutex> lk(t->mu);
+    if (probe(false)) { p.ok = true; return p; }     // filled while we waited
+    bool success;
+    const bool adjacent = g->findArc(s, d) != -1;
+    if (g->isComplete || (t->prefersDirectPaths && adjacent)) {
+        double lat, rel;
+        success = shdpe::host_direct_path(*g, s, d, &lat, &rel) == SHD_PE_OK;
+        if (success) store_path(t, true, s, d, lat, rel);
+    } else {
+        success = compute_source_paths(t, s, d);
     }
+    if (success && probe(true)) p.ok = true;
     return p;
 }
 
@@ -157,10 +135,12 @@ extern "C" int shd_topology_new(ShdPe* pe, int32_t prefersDirectPaths, ShdTopolo
     const int32_t T = shd_pe_num_attached(pe);
     t->attached.resize(T);
     shd_pe_attached(pe, t->attached.data());
+    const int rc = shd_rowstore_new(t->g->n, t->attached.data(), T, &t->store);
+    if (rc) { delete t; return rc; }
     t->rlat.resize(T);
     t->rrel.resize(T);
     t->rflags.resize(T);
-    t->rows.resize(T);
+    t->radj.resize(T);
     *out = t;
     return SHD_PE_OK;
 }
@@ -169,16 +149,16 @@ extern "C" void shd_topology_free(ShdTopology* t) { delete t; }
 
 extern "C" double shd_topology_get_latency(ShdTopology* t, int32_t s, int32_t d) {
     if (!t) return -1.0;
-    std::lock_guard<std::mutex> lk(t->mu);
-    const PathRef p = get_path_entry(t, s, d);
-    return p ? p.row->lat[p.j] : -1.0;
+    int32_t a, b;
+    const PathVal p = get_path_entry(t, s, d, &a, &b);
+    return p.ok ? p.lat : -1.0;
 }
 
 extern "C" double shd_topology_get_reliability(ShdTopology* t, int32_t s, int32_t d) {
     if (!t) return -1.0;
-    std::lock_guard<std::mutex> lk(t->mu);
-    const PathRef p = get_path_entry(t, s, d);
-    return p ? p.row->rel[p.j] : -1.0;
+    int32_t a, b;
+    const PathVal p = get_path_entry(t, s, d, &a, &b);
+    return p.ok ? p.rel : -1.0;
 }
 
 extern "C" int shd_topology_is_routable(ShdTopology* t, int32_t s, int32_t d) {
@@ -187,34 +167,29 @@ extern "C" int shd_topology_is_routable(ShdTopology* t, int32_t s, int32_t d) {
 
 extern "C" int shd_topology_increment_path_packet_counter(ShdTopology* t, int32_t s, int32_t d) {
     if (!t) return -1;
-    std::lock_guard<std::mutex> lk(t->mu);
-    const PathRef p = get_path_entry(t, s, d);
-    if (!p) return -1;
-    p.row->packets[p.j]++;
-    return 0;
+    int32_t a = -1, b = -1;
+    const PathVal p = get_path_entry(t, s, d, &a, &b);
+    if (!p.ok) return -1;
+    return shd_rowstore_increment(t->store, a, b);
 }
 
 extern "C" int shd_topology_cached(const ShdTopology* t, int32_t s, int32_t d, double* lat,
                                    double* rel, int32_t* isDirect, int64_t* packetCount) {
     if (!t) return 0;
-    if (s < 0 || s >= t->g->n || d < 0 || d >= t->g->n) return 0;
-    const PathRef p = cache_get(t, s, d);
-    if (!p) return 0;
-    if (lat) *lat = p.row->lat[p.j];
-    if (rel) *rel = p.row->rel[p.j];
-    if (isDirect) *isDirect = p.row->state[p.j] == 2 ? 1 : 0;
-    if (packetCount) *packetCount = p.row->packets[p.j];
+    uint64_t pc = 0;
+    if (!shd_rowstore_get(t->store, s, d, lat, rel, isDirect, &pc)) return 0;
+    if (packetCount) *packetCount = (int64_t)pc;
     return 1;
 }
 
 extern "C" double shd_topology_min_latency(const ShdTopology* t) {
-    return t ? t->minimumPathLatency : 0.0;
+    return t ? shd_rowstore_min_latency(t->store) : 0.0;
 }
 
 extern "C" int64_t shd_topology_cache_size(const ShdTopology* t) {
-    return t ? t->cacheSize : 0;
+    return t ? shd_rowstore_size(t->store) : 0;
 }
 
 extern "C" int64_t shd_topology_rows_computed(const ShdTopology* t) {
-    return t ? t->rowsComputed : 0;
+    return t ? t->rowsComputed.load(std::memory_order_relaxed) : 0;
 }

@@ -36,7 +36,9 @@ EXPORTS = [
     "shd_topology_is_routable", "shd_topology_increment_path_packet_counter",
     "shd_topology_cached", "shd_topology_min_latency", "shd_topology_cache_size",
     "shd_topology_rows_computed", "shd_graphml_parse", "shd_graphml_describe",
-    "shd_graphml_vertex_id", "shd_graphml_free",
+    "shd_graphml_vertex_id", "shd_graphml_free", "shd_rowstore_new", "shd_rowstore_free",
+    "shd_rowstore_get", "shd_rowstore_store", "shd_rowstore_store_row", "shd_rowstore_increment",
+    "shd_rowstore_size", "shd_rowstore_min_latency", "shd_rowstore_memory_bytes",
 ]
 
 
@@ -132,6 +134,15 @@ def load_library(path: str = LIB_PATH):
         "shd_graphml_describe": (C.c_int, [vp, vp, vp]),
         "shd_graphml_vertex_id": (C.c_char_p, [vp, i32]),
         "shd_graphml_free": (None, [vp]),
+        "shd_rowstore_new": (C.c_int, [i32, vp, i32, vp]),
+        "shd_rowstore_free": (None, [vp]),
+        "shd_rowstore_get": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
+        "shd_rowstore_store": (C.c_int, [vp, i32, i32, i32, i32, i32, f64, f64]),
+        "shd_rowstore_store_row": (C.c_int, [vp, i32, vp, vp, vp, i32, vp]),
+        "shd_rowstore_increment": (C.c_int, [vp, i32, i32]),
+        "shd_rowstore_size": (i64, [vp]),
+        "shd_rowstore_min_latency": (f64, [vp]),
+        "shd_rowstore_memory_bytes": (i64, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -329,6 +340,72 @@ class Engine:
         self._chk(self._lib.shd_pe_is_complete_device(self.h, C.byref(x)),
                   "shd_pe_is_complete_device")
         return bool(x.value)
+
+
+class RowStore:
+    """shd_rowstore_*: topology.c's path cache (:1284-1386) as a triangular
+    dense store; host only (no device)."""
+
+    def __init__(self, n_vertices: int, attached):
+        self._lib = load_library()
+        self._att = np.ascontiguousarray(attached, dtype=np.int32)
+        h = C.c_void_p()
+        rc = self._lib.shd_rowstore_new(int(n_vertices), _p(self._att), self._att.shape[0],
+                                        C.byref(h))
+        if rc:
+            raise EngineError(rc, "shd_rowstore_new")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.shd_rowstore_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def get(self, s, d):
+        """(lat, rel, isDirect, packetCount) stored under exactly (s, d), or None."""
+        lat, rel = C.c_double(), C.c_double()
+        isd, pc = C.c_int32(), C.c_uint64()
+        if not self._lib.shd_rowstore_get(self.h, int(s), int(d), C.byref(lat), C.byref(rel),
+                                          C.byref(isd), C.byref(pc)):
+            return None
+        return lat.value, rel.value, bool(isd.value), pc.value
+
+    def store(self, s, d, is_direct, is_complete, prefer_direct_and_adjacent, lat, rel) -> int:
+        rc = self._lib.shd_rowstore_store(self.h, int(s), int(d), int(is_direct),
+                                          int(is_complete), int(prefer_direct_and_adjacent),
+                                          float(lat), float(rel))
+        if rc < 0:
+            raise EngineError(rc, "shd_rowstore_store")
+        return rc
+
+    def store_row(self, s, lat, rel, flags, is_complete=False, adjacent=None) -> bool:
+        lat = np.ascontiguousarray(lat, dtype=np.float64)
+        rel = np.ascontiguousarray(rel, dtype=np.float64)
+        flags = np.ascontiguousarray(flags, dtype=np.uint8)
+        adj = None if adjacent is None else np.ascontiguousarray(adjacent, dtype=np.uint8)
+        rc = self._lib.shd_rowstore_store_row(self.h, int(s), _p(lat), _p(rel), _p(flags),
+                                              int(is_complete), _p(adj))
+        if rc < 0:
+            raise EngineError(rc, "shd_rowstore_store_row")
+        return rc == 1
+
+    def increment(self, s, d) -> int:
+        return self._lib.shd_rowstore_increment(self.h, int(s), int(d))
+
+    def size(self) -> int:
+        return self._lib.shd_rowstore_size(self.h)
+
+    def min_latency(self) -> float:
+        return self._lib.shd_rowstore_min_latency(self.h)
+
+    def memory_bytes(self) -> int:
+        return self._lib.shd_rowstore_memory_bytes(self.h)
 
 
 class TopologyShim:

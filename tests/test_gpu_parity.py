@@ -434,3 +434,52 @@ def test_batched_tie_rows_partial_targets(E, oracle_mod):
     att = np.arange(0, 3000, 5, dtype=np.int32)
     st = _check_engine(E, oracle_mod, top, att, force=5)
     assert st["mode"] == 1 and st["rowsTieEarly"] > 0
+
+
+def test_topology_shim_concurrent_readers(E, oracle_mod):
+    """8 host threads query the topology mirror at once (the reference's
+    worker threads): cache hits take no lock, misses serialise.  Every value
+    is the engine row entry of one of the two directions (whichever row was
+    computed first -- the reference's cache keeps the first), the cache
+    holds one entry per unordered pair, and packet counters add up."""
+    import threading
+    top = G.random_sparse(800, 5, seed=41, vloss=True)
+    att = np.arange(0, 800, 3, dtype=np.int32)
+    eng = E.Engine(top, att)
+    shim = E.TopologyShim(eng)
+    pos = {int(v): j for j, v in enumerate(att)}
+    eng.compute_rows(att)
+    rows = {int(s): eng.get_row(int(s)) for s in att}
+    errors, incs = [], [0] * 8
+
+    def worker(i):
+        r = np.random.default_rng(500 + i)
+        for _ in range(4000):
+            s, d = (int(x) for x in r.choice(att, 2))
+            if s == d:
+                continue
+            lat = shim.get_latency(s, d)
+            ok = (lat == rows[s]["lat"][pos[d]] or lat == rows[d]["lat"][pos[s]])
+            if not ok:
+                errors.append((s, d, lat))
+            if shim.increment(s, d) == 0:
+                incs[i] += 1
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
+    total, seen = 0, 0
+    for a in att:
+        for b in att:
+            c1, c2 = shim.cached(int(a), int(b)), shim.cached(int(b), int(a))
+            assert a == b or not (c1 and c2)
+            if c1:
+                total += c1[3]
+                seen += 1
+    assert total == sum(incs)
+    assert seen == shim.cache_size
+    shim.close()
+    eng.close()

@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "shd_pathengine.h")
 def _declared_symbols():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(shd_(?:pe|topology|graphml)_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(shd_(?:pe|topology|graphml|rowstore)_\w+)\s*\(", txt)))
 
 
 @pytest.fixture(scope="module")

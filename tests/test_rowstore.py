@@ -1,0 +1,180 @@
+"""shd_rowstore_* (pe_rowstore.cpp): topology.c's two-level path cache
+(_topology_getPathFromCache :1284-1305, _topology_shouldStorePath
+:1307-1336, _topology_storePathInCache :1338-1386) as a triangular dense
+store.  Checked here (CPU, no device) against a literal dict model of the
+reference's GHashTable<src, GHashTable<dst, Path*>>, and under concurrent
+readers."""
+import threading
+
+import numpy as np
+import pytest
+
+from shdpe.engine import RowStore, F_NOEDGE, F_UNREACHABLE
+
+
+class RefCache:
+    """The reference cache, restated with dicts (topology.c:1284-1386)."""
+
+    def __init__(self):
+        self.c = {}
+        self.min_lat = 0.0
+
+    def get(self, s, d):
+        return self.c.get(s, {}).get(d)
+
+    def should_store(self, is_direct, s, d, is_complete, adjacent_pref):
+        if self.get(s, d) is not None or self.get(d, s) is not None:
+            return False
+        if is_complete and not is_direct:
+            return False
+        if adjacent_pref and not is_direct:
+            return False
+        return True
+
+    def store(self, s, d, is_direct, is_complete, adjacent_pref, lat, rel):
+        if not self.should_store(is_direct, s, d, is_complete, adjacent_pref):
+            return 0
+        self.c.setdefault(s, {})[d] = [lat, rel, bool(is_direct), 0]
+        if self.min_lat == 0 or lat < self.min_lat:
+            self.min_lat = lat
+        return 1
+
+
+def _attached(n, k, seed):
+    rng = np.random.default_rng(seed)
+    return np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_store_get_semantics_match_reference_cache(seed):
+    n, k = 300, 120
+    att = _attached(n, k, seed)
+    st, ref = RowStore(n, att), RefCache()
+    rng = np.random.default_rng(seed)
+    for _ in range(6000):
+        s, d = (int(x) for x in rng.choice(att, 2))
+        if rng.random() < 0.1:
+            d = s
+        is_direct = bool(rng.random() < 0.2)
+        is_complete = bool(rng.random() < 0.05)
+        adj = bool(rng.random() < 0.1)
+        lat, rel = float(rng.uniform(1, 100)), float(rng.uniform(0.9, 1))
+        assert st.store(s, d, is_direct, is_complete, adj, lat, rel) == \
+            ref.store(s, d, is_direct, is_complete, adj, lat, rel)
+        if rng.random() < 0.3:
+            a, b = (int(x) for x in rng.choice(att, 2))
+            e = ref.get(a, b)
+            if e is not None:
+                e[3] += 1
+            assert st.increment(a, b) == (0 if e is not None else -1)
+    for s in att:
+        for d in att:
+            e, g = ref.get(int(s), int(d)), st.get(s, d)
+            assert (e is None) == (g is None), (s, d)
+            if e is not None:
+                assert g == tuple(e)
+    assert st.size() == sum(len(v) for v in ref.c.values())
+    assert st.min_latency() == ref.min_lat
+    # one slot per unordered pair at most, allocated per touched row
+    assert st.memory_bytes() <= (k * (k + 1) // 2) * 25 + k * 8 + n * 4
+
+
+def test_unattached_and_invalid_ids():
+    st = RowStore(10, np.array([1, 3, 5], np.int32))
+    assert st.get(0, 1) is None and st.get(-1, 3) is None and st.get(3, 99) is None
+    assert st.increment(1, 2) == -1
+    with pytest.raises(Exception):
+        st.store(1, 2, 0, 0, 0, 1.0, 1.0)
+    assert st.store(1, 3, 0, 0, 0, 2.0, 0.5) == 1
+    assert st.get(1, 3) == (2.0, 0.5, False, 0) and st.get(3, 1) is None
+    assert st.store(3, 1, 1, 0, 0, 9.0, 0.1) == 0          # reverse direction cached
+    with pytest.raises(Exception):
+        RowStore(10, np.array([1, 1], np.int32))            # duplicate attached vertex
+
+
+def test_store_row_follows_row_loop():
+    """topology.c:1815-1859 over one engine row: unreachable skipped, failed
+    fold skipped + isAllSuccess cleared, adjacency under prefersDirectPaths."""
+    att = np.array([2, 4, 6, 8], np.int32)
+    st, ref = RowStore(10, att), RefCache()
+    lat = np.array([1.0, 2.0, 3.0, 4.0])
+    rel = np.array([0.9, 0.8, 0.7, 0.6])
+    flags = np.array([0, F_UNREACHABLE, 0, 0], np.uint8)
+    adj = np.array([0, 0, 1, 0], np.uint8)
+    assert st.store_row(4, lat, rel, flags, False, adj) is True
+    for j, t in enumerate(att):
+        if not flags[j]:
+            ref.store(4, int(t), False, False, bool(adj[j]), lat[j], rel[j])
+    for t in att:
+        e, g = ref.get(4, int(t)), st.get(4, t)
+        assert (e is None) == (g is None) and (e is None or g == tuple(e))
+    flags2 = np.array([0, 0, F_NOEDGE, 0], np.uint8)
+    assert st.store_row(8, lat, rel, flags2) is False
+    assert st.store_row(2, lat, rel, np.zeros(4, np.uint8), True) is True   # complete: nothing
+    assert st.get(2, 6) is None
+
+
+def test_concurrent_readers_and_writer():
+    """8 reader threads probe and count packets while a writer inserts rows;
+    every value a reader sees is the one stored, counters add up."""
+    n, k = 2000, 400
+    att = _attached(n, k, 7)
+    st = RowStore(n, att)
+    rng = np.random.default_rng(7)
+    lat = rng.uniform(1, 100, size=(k, k))
+    rel = rng.uniform(0.5, 1, size=(k, k))
+    stop = threading.Event()
+    errors, incs = [], [0] * 8
+
+    def reader(i):
+        r = np.random.default_rng(100 + i)
+        while not stop.is_set():
+            a, b = (int(x) for x in r.integers(0, k, 2))
+            g = st.get(att[a], att[b])
+            if g is not None:
+                if g[0] not in (lat[a, b], lat[b, a]) or g[1] not in (rel[a, b], rel[b, a]):
+                    errors.append((a, b, g))
+                if st.increment(att[a], att[b]) == 0:
+                    incs[i] += 1
+
+    th = [threading.Thread(target=reader, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for a in range(k):
+        st.store_row(att[a], lat[a], rel[a], np.zeros(k, np.uint8))
+    stop.set()
+    for t in th:
+        t.join()
+    assert not errors
+    assert st.size() == k * (k + 1) // 2
+    total = 0
+    for a in range(k):
+        for b in range(a, k):
+            g = st.get(att[a], att[b])
+            assert g is not None and g[0] == lat[a, b] and g[1] == rel[a, b]
+            total += g[3]
+    assert total == sum(incs)
+
+
+def test_rowstore_under_thread_sanitizer(tmp_path):
+    """pe_rowstore.cpp built with -fsanitize=thread (host code), readers racing
+    a writer: no data race reported, counters and values consistent."""
+    import os
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    exe = str(tmp_path / "rowstore_race")
+    cmd = [gxx, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+           "-I", os.path.join(root, "include"),
+           os.path.join(root, "tests", "native", "rowstore_race.cpp"),
+           os.path.join(root, "shadow-1_amd", "csrc", "pe_rowstore.cpp"), "-o", exe]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    if b.returncode != 0 and "tsan" in (b.stderr or "").lower():
+        pytest.skip("ThreadSanitizer runtime unavailable")
+    assert b.returncode == 0, b.stderr[-2000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout, r.stderr[-3000:])
