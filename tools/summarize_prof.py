@@ -34,11 +34,25 @@ json.dump(out, open(os.path.join(dst, f"{tag}_{wl}_pmc.json"), "w"), indent=1)
 if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
     fetch = pmc["FETCH_SIZE"]["per_dispatch"] * 1024
     write = pmc["WRITE_SIZE"]["per_dispatch"] * 1024
-    traffic = {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+    # k_batch_rows reads [v][LB] lines with 16-lane groups: the calibrated
+    # shape (random 128-B lines report exactly half).  Other kernels read
+    # narrower pieces, where one request may move 64 or 128 B: FETCH_SIZE as
+    # is (lower bound), 2x as the upper bound.
+    lines = kern == "k_batch_rows"
+    read = 2 * fetch if lines else fetch
+    traffic = {"bytes_per_launch": read + write, "read_bytes": read,
+               "read_bytes_upper": 2 * fetch, "fetch_size_bytes": fetch, "write_bytes": write,
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, "
-                         "KB*1024, bench.py --steps 1 (one launch). FETCH_SIZE is not doubled: "
-                         "the 1/2 correction of MI355X_MICROARCH.md applies to 16-B/lane "
-                         "streaming reads; this kernel's reads are 4-8 B scattered (uncalibrated).",
+                         "KB*1024, bench.py --steps 1 (one launch).  "
+                         + ("Reads = 2 x FETCH_SIZE: calibrated on gfx950 for this kernel's "
+                            "dominant read shape (random 128-B lines read by 16-lane groups "
+                            "report exactly half, like 16-B/lane streaming; "
+                            "profiles/r02e_fetch_calibration.json).  " if lines else
+                            "Reads = FETCH_SIZE (lower bound; 64- or 128-B requests cannot be "
+                            "told apart, read_bytes_upper = 2 x).  ")
+                         + "Writes = WRITE_SIZE (exact in the same calibration).  EA requests "
+                           "include Infinity-Cache hits: L2-miss traffic, an upper bound on "
+                           "HBM bytes.",
                "tag": tag}
     json.dump(traffic, open(os.path.join(dst, f"traffic_{wl}.json"), "w"), indent=1)
 print(json.dumps({k: v["per_dispatch"] for k, v in pmc.items()}, indent=1))
