@@ -483,3 +483,31 @@ def test_topology_shim_concurrent_readers(E, oracle_mod):
     assert seen == shim.cache_size
     shim.close()
     eng.close()
+
+
+@pytest.mark.parametrize("n,ok", [(520_000, True), (530_000, False)])
+def test_vertex_limit_of_batched_kernel(E, oracle_mod, n, ok):
+    """k_batch_rows keeps two pending bitmaps + the depth histogram in LDS:
+    about 523.9k vertices fit 160 KB.  Past that, shd_pe_create refuses the
+    graph with SHD_PE_ETOOBIG instead of failing every later launch."""
+    rng = np.random.default_rng(n)
+    perm = rng.permutation(n)
+    extra = rng.integers(0, n, size=(n, 2))
+    src = np.concatenate([perm[:-1], extra[:, 0]])
+    dst = np.concatenate([perm[1:], extra[:, 1]])
+    key = np.minimum(src, dst).astype(np.int64) * n + np.maximum(src, dst)
+    _, first = np.unique(key, return_index=True)
+    keep = np.zeros(src.shape[0], bool)
+    keep[first] = True
+    keep &= src != dst
+    src, dst = src[keep], dst[keep]
+    top = Topology(n, False, src, dst, rng.uniform(1.0, 50.0, src.shape[0]),
+                   rng.uniform(0.0, 0.02, src.shape[0]))
+    att = np.array([0, n // 2, n - 1], np.int32)
+    if ok:
+        st = _check_engine(E, oracle_mod, top, att)
+        assert st["mode"] == 1 and st["batched"] == 1
+    else:
+        with pytest.raises(E.EngineError) as ei:
+            E.Engine(top, att)
+        assert ei.value.code == E.ETOOBIG
