@@ -245,6 +245,14 @@ def main():
         out["roofline"]["stream_GBps"] = sbw
         if bound == "hbm":
             out["roofline"]["frac_of_stream"] = achieved / sbw
+            tb = out["roofline"]["traffic"]
+            if tb and world == 1:
+                # measured L2-miss bytes (PMC, profiles/traffic_<wl>.json) over
+                # this run's launch time: how close the kernel runs to the
+                # bandwidth it actually moves
+                out["roofline"]["traffic_GBps"] = tb / (avg_launch_ms * 1e-3) / 1e9
+                out["roofline"]["traffic_frac_of_stream"] = out["roofline"]["traffic_GBps"] / sbw
+                out["roofline"]["traffic_over_algorithmic"] = tb / bytes_per_launch
     if gather:
         out["allgather"] = gather
     if d2h:
