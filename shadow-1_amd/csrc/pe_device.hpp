@@ -154,9 +154,12 @@ struct SparseLaunch {
 };
 
 // kernels (pe_kernels.hip); all launched on `stream`.
+// rowAmbig[i]: 0 fast path, 1 full heap emulation, 2 + k tie data in slot k
+// of *dTie (device copy; null disables the export)
 void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
-                        const SparseLaunch& cfg, int32_t* dDbg, void* stream);
+                        const SparseLaunch& cfg, int32_t* dDbg, const TieBuf* dTie,
+                        void* stream);
 // dSlots (may be null): per exact row its tie slot (-1 = full emulation);
 // rows with a slot stop at the slot's threshold and leave their final
 // parents in tie.P for launch_tie_write

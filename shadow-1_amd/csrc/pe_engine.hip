@@ -70,6 +70,7 @@ struct Shard {
     int32_t* dSlots = nullptr;      // per exact row its tie slot, -1 full emulation
     TieBuf* dTie = nullptr;         // device copy of `tie` (k_batch_rows reads it)
     long long* dXdbg = nullptr;     // exact-kernel counters (SHD_PE_DEBUG_COUNTERS)
+    bool tieTried = false;
     double *dW = nullptr, *dRl = nullptr, *dD = nullptr;
     int32_t* dP = nullptr;
     uint8_t *dRowA = nullptr, *dRowB = nullptr, *dRowAmbD = nullptr, *dChunkEpoch = nullptr;
@@ -616,6 +617,34 @@ static int ensure_table(ShdPe* pe, Shard* sh) {
     return SHD_PE_OK;
 }
 
+// Tie slots for the early-stop emulation (both sparse paths): D f64 + P i32
+// + H i32 + R f64 per vertex, <= 2 GiB, <= 254 slots (rowAmbig stores
+// 2 + slot in a byte); arc indices carry TIE_AMB in bit 30.
+static int ensure_tie(ShdPe* pe, Shard* sh) {
+    if (sh->dTie || sh->tieTried) return SHD_PE_OK;
+    sh->tieTried = true;
+    int rc;
+    const size_t perTie = (size_t)pe->hg.n * 24;
+    size_t cap = std::min<size_t>({(size_t)254, (size_t)sh->rowsCap, ((size_t)2 << 30) / perTie});
+    if (pe->hg.nArcs() >= ((int64_t)1 << 30)) cap = 0;
+    if (cap > 0) {
+        void *td, *tp, *th, *tr, *tt, *tc, *sl, *dd;
+        const size_t cn = cap * (size_t)pe->hg.n;
+        if ((rc = dev_alloc(sh, &td, cn * 8)) || (rc = dev_alloc(sh, &tp, cn * 4)) ||
+            (rc = dev_alloc(sh, &th, cn * 4)) || (rc = dev_alloc(sh, &tr, cn * 8)) ||
+            (rc = dev_alloc(sh, &tt, cap * 8)) || (rc = dev_alloc(sh, &tc, 16)) ||
+            (rc = dev_alloc(sh, &sl, (size_t)sh->rowsCap * 4)) ||
+            (rc = dev_alloc(sh, &dd, sizeof(TieBuf))))
+            return rc;
+        sh->tie = TieBuf{(int32_t)cap, (int32_t*)tc, (double*)td, (int32_t*)tp, (double*)tt,
+                         (int32_t*)th, (double*)tr, (int64_t)pe->hg.n};
+        sh->dSlots = (int32_t*)sl;
+        sh->dTie = (TieBuf*)dd;
+        HIPCHK(hipMemcpy(sh->dTie, &sh->tie, sizeof(TieBuf), hipMemcpyHostToDevice));
+    }
+    return SHD_PE_OK;
+}
+
 static int ensure_batch(ShdPe* pe, Shard* sh) {
     if (sh->batchReady) return SHD_PE_OK;
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
@@ -645,26 +674,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.nStride = (int64_t)NS;
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
-    // tie slots: D f64 + P i32 + H i32 + R f64 per vertex, <= 2 GiB, <= 254
-    // (rowAmbig stores 2 + slot in a byte); arc indices carry TIE_AMB in bit 30
-    const size_t perTie = (size_t)pe->hg.n * 24;
-    size_t cap = std::min<size_t>({(size_t)254, (size_t)sh->rowsCap, ((size_t)2 << 30) / perTie});
-    if (pe->hg.nArcs() >= ((int64_t)1 << 30)) cap = 0;
-    if (cap > 0) {
-        void *td, *tp, *th, *tr, *tt, *tc, *sl, *dd;
-        const size_t cn = cap * (size_t)pe->hg.n;
-        if ((rc = dev_alloc(sh, &td, cn * 8)) || (rc = dev_alloc(sh, &tp, cn * 4)) ||
-            (rc = dev_alloc(sh, &th, cn * 4)) || (rc = dev_alloc(sh, &tr, cn * 8)) ||
-            (rc = dev_alloc(sh, &tt, cap * 8)) || (rc = dev_alloc(sh, &tc, 16)) ||
-            (rc = dev_alloc(sh, &sl, (size_t)sh->rowsCap * 4)) ||
-            (rc = dev_alloc(sh, &dd, sizeof(TieBuf))))
-            return rc;
-        sh->tie = TieBuf{(int32_t)cap, (int32_t*)tc, (double*)td, (int32_t*)tp, (double*)tt,
-                         (int32_t*)th, (double*)tr, (int64_t)pe->hg.n};
-        sh->dSlots = (int32_t*)sl;
-        sh->dTie = (TieBuf*)dd;
-        HIPCHK(hipMemcpy(sh->dTie, &sh->tie, sizeof(TieBuf), hipMemcpyHostToDevice));
-    }
+    if ((rc = ensure_tie(pe, sh))) return rc;
     sh->batchReady = true;
     return SHD_PE_OK;
 }
@@ -874,9 +884,11 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 print_batch_debug(pe, sh, dbg.data(), nB);
             }
         } else {
+            if ((rc = ensure_tie(pe, sh))) return rc;
+            if (sh->dTie) HIPCHK(hipMemsetAsync(sh->tie.count, 0, 4, sh->stream));
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_sparse_rows(sh->dg, sh->tab, sh->sc, sh->dRows, cnt, sh->dRowAmbig, sh->cfg,
-                               sh->dDbg, sh->stream);
+                               sh->dDbg, sh->dTie, sh->stream);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(sh->evB, sh->stream));
             amb.resize(cnt);
@@ -885,8 +897,22 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             HIPCHK(hipStreamSynchronize(sh->stream));
             st.msSparseKernel += elapsed(sh->evA, sh->evB);
             st.launchesSparse++;
-            for (int32_t i = 0; i < cnt; ++i)
-                if (amb[i]) exactRows.push_back(pos[c0 + i]);
+            fullRows.clear();
+            for (int32_t i = 0; i < cnt; ++i) {
+                if (!amb[i]) continue;
+                if (amb[i] >= 2) {
+                    exactRows.push_back(pos[c0 + i]);
+                    exactSlots.push_back(amb[i] - 2);
+                } else {
+                    fullRows.push_back(pos[c0 + i]);
+                }
+            }
+            if (!exactSlots.empty()) {
+                exactRows.insert(exactRows.end(), fullRows.begin(), fullRows.end());
+                exactSlots.resize(exactRows.size(), -1);
+            } else {
+                exactRows.swap(fullRows);
+            }
             if (sh->dDbg) {
                 std::vector<int32_t> dbg((size_t)cnt * 16);
                 HIPCHK(hipMemcpy(dbg.data(), sh->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));

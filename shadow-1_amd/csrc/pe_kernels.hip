@@ -366,7 +366,7 @@ template <int LAYOUT, int LPV>
 __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
     DevGraph g0, DevTable tab0, DevScratch sc0, const int32_t* __restrict__ rows, int32_t nRows,
     uint8_t* rowAmbig, double delta, int32_t qcap, int32_t hcap, int32_t heavyDeg, int32_t* dbg,
-    int32_t kflags) {
+    int32_t kflags, const TieBuf* __restrict__ tieDesc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
@@ -712,14 +712,21 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                         if (a + k < a1) {
                             const unsigned long long dub = du[k];
                             if (dub <= dvb && b2d(dub) + lw[k] == dv) {
-                                if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
                                 if (dub < best) { best = dub; cnt = 1; ba = a + k; bu = cu[k]; }
                                 else if (dub == best) ++cnt;
                             }
                         }
                     }
                 }
-                if (cnt != 1) { myAmb = 1; if (ba < 0) { c.P[v] = -1; continue; } }
+                // the heap decides: equal-minimum tight predecessors, or the
+                // minimum one reaching v by a zero-increment arc (a farther
+                // zero-increment predecessor cannot win).  Marked in P's bit
+                // 30 for the tie export (the row then never uses P itself).
+                if (cnt != 1 || best == dvb) {
+                    myAmb = 1;
+                    c.P[v] = TIE_AMB | (ba > 0 ? ba : 0);
+                    continue;
+                }
                 c.P[v] = ba;
                 if ((int)c.H[v] != (int)c.H[bu] + 1 || c.R[v] != c.R[bu] * g.inRel[ba]) myMis = 1;
             }
@@ -762,7 +769,6 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                             if (!ok[k]) continue;
                             const unsigned long long dub = du[k];
                             if (dub <= dvb && b2d(dub) + lw[k] == dv) {
-                                if (dub == dvb) myAmb = 1;     // zero-increment edge: pop order
                                 if (dub < best) { best = dub; cnt = 1; ba = ab + k * PL; bu = cu[k]; }
                                 else if (dub == best) ++cnt;
                             }
@@ -783,7 +789,11 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
                 }
                 if (sub != 0 || !inV) continue;
                 if (!act) { c.P[v] = -1; continue; }
-                if (cnt != 1) { myAmb = 1; if (ba < 0) { c.P[v] = -1; continue; } }
+                if (cnt != 1 || best == dvb) {
+                    myAmb = 1;
+                    c.P[v] = TIE_AMB | (ba > 0 ? ba : 0);
+                    continue;
+                }
                 c.P[v] = ba;
                 if ((int)c.H[v] != (int)c.H[bu] + 1 || c.R[v] != c.R[bu] * g.inRel[ba]) myMis = 1;
             }
@@ -809,7 +819,45 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
             dbg[16 * b + 15] = (int)pst[3];
         }
         if (ctl->ambig) {
-            if (tid == 0) rowAmbig[b] = 1;
+            // tie export (as k_batch_rows): final distances, fast-path parents
+            // with the ambiguous ones marked, and the largest tied
+            // predecessor distance -> early-stop emulation + k_tie_write
+            int sl = -1;
+            if (tieDesc) {
+                const TieBuf tie = *tieDesc;
+                if (tid == 0) {
+                    const int x = atomicAdd(tie.count, 1);
+                    ctl->changed = x < tie.cap ? x : -1;
+                    ctl->minNext[0] = 0ull;
+                }
+                __syncthreads();
+                sl = ctl->changed;
+                if (sl >= 0) {
+                    unsigned long long thr = 0ull;
+                    const bool undirected = g.inCol == g.col;
+                    const size_t o0 = (size_t)sl * (size_t)tie.n;
+                    for (int v = tid; v < n; v += NT) {
+                        const unsigned long long dvb = c.dist[v];
+                        const int pv = v == s ? -1 : c.P[v];
+                        tie.D[o0 + v] = b2d(dvb);
+                        tie.P[o0 + v] = pv;
+                        if (pv >= 0 && (pv & TIE_AMB)) {   // rare: the tied distance
+                            const int a0 = undirected ? c.rp[v] : g.inPtr[v];
+                            const int a1 = undirected ? c.rp[v + 1] : g.inPtr[v + 1];
+                            unsigned long long mt = INF_BITS;
+                            for (int a = a0; a < a1; ++a) {
+                                const unsigned long long du = c.dist[g.inCol[a]];
+                                if (du <= dvb && d2b(b2d(du) + g.inLat[a]) == dvb && du < mt) mt = du;
+                            }
+                            if (mt != INF_BITS && mt > thr) thr = mt;
+                        }
+                    }
+                    if (thr) atomicMax(&ctl->minNext[0], thr);
+                    __syncthreads();
+                    if (tid == 0) tie.thr[sl] = b2d(ctl->minNext[0]);
+                }
+            }
+            if (tid == 0) rowAmbig[b] = sl >= 0 ? (uint8_t)(2 + sl) : (uint8_t)1;
             __syncthreads();
             continue;
         }
@@ -1509,44 +1557,47 @@ int sparse_max_threads() { return SP_THREADS; }
 template <int L, int LPV>
 static void launch_sparse_lpv(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                               const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
-                              const SparseLaunch& cfg, int32_t* dDbg, hipStream_t st, int grid) {
+                              const SparseLaunch& cfg, int32_t* dDbg, const TieBuf* dTie,
+                              hipStream_t st, int grid) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sparse_rows<L, LPV>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
     hipLaunchKernelGGL((k_sparse_rows<L, LPV>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st,
                        g, tab, sc, dRows, nRows, dRowAmbig, cfg.delta, cfg.qcap, cfg.hcap,
-                       cfg.heavyDeg, dDbg, cfg.kflags);
+                       cfg.heavyDeg, dDbg, cfg.kflags, dTie);
 }
 
 template <int L>
 static void launch_sparse_layout(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                                  const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
-                                 const SparseLaunch& cfg, int32_t* dDbg, hipStream_t st, int grid) {
+                                 const SparseLaunch& cfg, int32_t* dDbg, const TieBuf* dTie,
+                                 hipStream_t st, int grid) {
     if constexpr (L == 3) {
         const int sel = (cfg.kflags >> 4) & 3;
         if (sel == 1)
-            return launch_sparse_lpv<L, 2>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+            return launch_sparse_lpv<L, 2>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
         if (sel == 2)
-            return launch_sparse_lpv<L, 1>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+            return launch_sparse_lpv<L, 1>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
         if (sel == 3)
-            return launch_sparse_lpv<L, 8>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+            return launch_sparse_lpv<L, 8>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
     }
-    launch_sparse_lpv<L, 4>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+    launch_sparse_lpv<L, 4>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
 }
 
 void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, uint8_t* dRowAmbig,
-                        const SparseLaunch& cfg, int32_t* dDbg, void* stream) {
+                        const SparseLaunch& cfg, int32_t* dDbg, const TieBuf* dTie,
+                        void* stream) {
     if (nRows <= 0) return;
     const int grid = nRows < cfg.grid ? nRows : cfg.grid;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (cfg.layout == 3)
-        launch_sparse_layout<3>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+        launch_sparse_layout<3>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
     else if (cfg.layout == 2)
-        launch_sparse_layout<2>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+        launch_sparse_layout<2>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
     else if (cfg.layout == 1)
-        launch_sparse_layout<1>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+        launch_sparse_layout<1>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
     else
-        launch_sparse_layout<0>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, st, grid);
+        launch_sparse_layout<0>(g, tab, sc, dRows, nRows, dRowAmbig, cfg, dDbg, dTie, st, grid);
 }
 
 void launch_tie_scan(const DevGraph& g, const int32_t* dRows, const int32_t* dSlots,

@@ -91,6 +91,7 @@ def test_quantized_ties_use_exact_kernel(E, oracle_mod):
     top = G.random_sparse(400, 6, seed=9, quantum=1.0)
     st = _check_engine(E, oracle_mod, top, np.arange(400))
     assert st["rowsExact"] > 0
+    assert st["rowsTieEarly"] > 0      # k_sparse_rows tie export -> early stop
 
 
 def test_forced_exact_kernel_all_rows(E, oracle_mod):
