@@ -1056,6 +1056,14 @@ __global__ __launch_bounds__(TW_THREADS) void k_tie_write(DevGraph g0, DevTable 
 // the global slot.
 extern __shared__ __attribute__((aligned(16))) unsigned char ex_smem[];
 
+// a uniform lane's double, by two v_readlane (no LDS round trip)
+__device__ __forceinline__ double readlane_f64(double x, int k) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, k);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), k);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 struct WHeap {
     double* gkey;     // global tail: position p >= hc at gkey[p - hc]
     int32_t* gidx;
@@ -1118,12 +1126,16 @@ struct WHeap {
         const bool lds = (head + 1) * (1 << dd) + (1 << dd) - 2 < hc;   // deepest node of the round
         double kq = 0.0;
         int iq = -1;
-        if (lds) {
-            if (valid) { kq = lkey()[pos]; iq = lidx()[pos]; }
+        if (lds) {                                         // branch-free: clamped position
+            const int pc = valid ? pos : 0;
+            kq = lkey()[pc];
+            iq = lidx()[pc];
         } else if (valid) {
             get(pos, kq, iq);
         }
-        const double ks = __shfl_xor(kq, 1, 64);           // sibling (lanes 2i, 2i+1)
+        // sibling (lanes 2i, 2i+1): a DPP quad permute, no LDS round trip
+        const double ks = __longlong_as_double(
+            (long long)gxor64<4>((unsigned long long)__double_as_longlong(kq), 1));
         // the child its parent descends to: left when left >= right or no right
         const bool chosen = valid && (left ? (!sibValid || kq >= ks) : !(ks >= kq));
         const unsigned long long cm = __ballot(chosen);
@@ -1146,7 +1158,7 @@ struct WHeap {
             if (lane == 0) put(head, k, id);
             return true;
         }
-        const int hp = __shfl(pos, 63 - __builtin_clzll(mm), 64);   // deepest node passed
+        const int hp = __builtin_amdgcn_readlane(pos, 63 - __builtin_clzll(mm));   // deepest passed
         if (__builtin_popcountll(mm) < dd) {
             if (lane == 0) put(hp, k, id);
             return true;
@@ -1163,7 +1175,9 @@ struct WHeap {
         double ka = 0.0;
         int ia = -1;
         if (lds) {
-            if (valid) { ka = lkey()[a]; ia = lidx()[a]; }
+            const int ac = valid ? a : 0;
+            ka = lkey()[ac];
+            ia = lidx()[ac];
         } else if (valid) {
             get(a, ka, ia);
         }
@@ -1321,7 +1335,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                     mask &= mask - 1;
                     const int vk = __builtin_amdgcn_readlane(v, k);
                     const int nk = __builtin_amdgcn_readlane(need, k);
-                    const double ak = __shfl(alt, k, 64);
+                    const double ak = readlane_f64(alt, k);
                     if (nk == 1) {                    // igraph_2wheap_push_with_index
                         h.shift_up(size, -ak, vk, lane);
                         size += 1;
@@ -1482,7 +1496,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
                     mask &= mask - 1;
                     const int vk = __builtin_amdgcn_readlane(v, k);
                     const int nk = __builtin_amdgcn_readlane(need, k);
-                    const double ak = __shfl(alt, k, 64);
+                    const double ak = readlane_f64(alt, k);
                     if (lane == 0) {
                         if (nk == 1) {            // igraph_2wheap_push_with_index
                             shift_up(size, -ak, vk);
