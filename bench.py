@@ -105,7 +105,7 @@ def main():
                          "share is 16 CPUs, os.cpu_count() there shows the whole machine)")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the device-copy HBM bandwidth reference")
-    ap.add_argument("--tie-stress", default="c2q,c4q",
+    ap.add_argument("--tie-stress", default="c2q,c4q,c5q",
                     help="comma list of quantised variants timed after the headline (rank 0, "
                          "N=1; '' = off): their tie-row fraction and k_exact_rows time")
     ap.add_argument("--d2h-rows", type=int, default=2048,
@@ -294,6 +294,7 @@ def tie_stress(workload, steps, dbg):
     return {"workload": workload, "rows": int(eng.T), "ms_per_step": el * 1e3,
             "rows_per_s": eng.T / el, "tie_rows": st["rowsExact"] // k,
             "tie_row_fraction": st["rowsExact"] / k / eng.T,
+            "tie_rows_early_stop": st["rowsTieEarly"] // k,
             "ms_exact_kernel_per_step": st["msExactKernel"] / k,
             "ms_main_kernel_per_step": (st["msSparseKernel"] + st["msDenseKernel"]) / k}
 

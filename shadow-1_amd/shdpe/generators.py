@@ -208,6 +208,7 @@ CONFIGS = {
     "c3a": dict(desc="dense n=20k complete (configs[2], direct rows)"),
     "c3b": dict(desc="dense n=20k minus one edge (configs[2], min-plus)"),
     "c5": dict(desc="BA n=250k m=2, 65,536 attached (configs[4])"),
+    "c5q": dict(desc="C5 with latencies rounded to 0.005 ms (tie stress, SURVEY.md 8d)"),
 }
 
 
@@ -219,7 +220,7 @@ def make_config(name: str):
     c2   RGG 10k, all sources        c2q  same, latencies rounded to 0.005
     c3a  dense 20k complete           c3b  dense 20k minus one edge
     c4   BA 100k, 16,384 attached     c4q  same, latencies rounded to 0.005
-    c5   BA 250k, 65,536 attached
+    c5   BA 250k, 65,536 attached     c5q  same, latencies rounded to 0.005
     """
     if name in ("c1", "c1m"):
         import os
@@ -243,7 +244,7 @@ def make_config(name: str):
     if name in ("c4", "c4q"):
         top = power_law(100_000, m=3, seed=4, quantum=0.005 if name == "c4q" else 0.0)
         return top, sample_attached(top.n, 16_384, seed=5)
-    if name == "c5":
-        top = power_law(250_000, m=2, seed=6)
+    if name in ("c5", "c5q"):
+        top = power_law(250_000, m=2, seed=6, quantum=0.005 if name == "c5q" else 0.0)
         return top, sample_attached(top.n, 65_536, seed=7)
     raise KeyError(name)

@@ -95,19 +95,42 @@ def test_c5_full_size(E, oracle_mod):
 
 
 def test_c4q_quantised_ties(E, oracle_mod):
-    """C4 with latencies rounded to 0.005 ms (like the shipped data): tie
-    rows go to k_exact_rows; 256 rows bit-exact against the oracle's
-    igraph-heap order."""
+    """C4 with latencies rounded to 0.005 ms (like the shipped data): the
+    whole table on the GPU; EVERY tie row (found by its F_EXACT flags:
+    early-stop emulation + k_tie_write, or cleared by the relevance scan)
+    plus 32 random rows bit-exact against the oracle's igraph-heap order."""
     top, att = G.make_config("c4q")
+    eng = E.Engine(top, att)
+    eng.compute_all()
+    st = eng.stats()
+    T = eng.T
+    tie_pos = []
+    for start in range(0, T, 1024):
+        blk = eng.get_rows(start, min(1024, T - start))
+        tie_pos += list(start + np.flatnonzero((blk["flags"] & E.F_EXACT).any(axis=1)))
+        del blk
+    assert st["rowsExact"] > 0 and st["rowsTieEarly"] > 0
+    # rows the relevance scan cleared keep fast-path parents and no F_EXACT
+    assert 0 < len(tie_pos) <= st["rowsExact"]
     rng = np.random.default_rng(3)
-    sample = np.sort(rng.choice(att, 256, replace=False))
+    sample = np.unique(np.concatenate([eng.attached[tie_pos], rng.choice(att, 32, replace=False)]))
+    exp, _ = _oracle_rows_async(oracle_mod, top, sample, att)()
+    _compare_sampled(eng, exp, sample, "c4q")
+    eng.close()
+
+
+def test_c5q_quantised_ties_sampled(E, oracle_mod):
+    """C5 with latencies rounded to 0.005 ms: 384 random rows on the GPU
+    (tie rows among them take the early-stop path) bit-exact against the
+    oracle."""
+    top, att = G.make_config("c5q")
+    rng = np.random.default_rng(5)
+    sample = np.sort(rng.choice(att, 384, replace=False))
     join = _oracle_rows_async(oracle_mod, top, sample, att)
     eng = E.Engine(top, att)
     eng.compute_rows(sample)
-    st = eng.stats()
     exp, _ = join()
-    _compare_sampled(eng, exp, sample, "c4q")
-    assert st["rowsExact"] > 0
+    _compare_sampled(eng, exp, sample, "c5q")
     eng.close()
 
 
