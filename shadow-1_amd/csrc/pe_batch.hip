@@ -24,13 +24,14 @@
 //      SURVEY.md Appendix B);
 //   2. predecessor pass: tight in-arc with minimum dist[u] per lane = igraph's
 //      first-popped tight predecessor; equal minima (or a zero-increment arc)
-//      make the row a tie row for k_exact_rows;
-//   3. hop counts = depth in the predecessor forest, by pointer jumping
-//      (exact integer sums, log2(depth) rounds);
-//   4. reliability in depth order: entries bucketed by depth (counting sort
-//      in LDS), then level by level R[v] = R[parent] * rel(parent, v) -- the
-//      reference's left fold (topology.c:1430, :1499) exactly;
-//   5. the row writer (topology.c:1805-1864).
+//      mark the entry ambiguous (the row becomes a tie row for k_exact_rows
+//      if a target's path meets it);
+//   3. labels on demand + the row writer (topology.c:1805-1864): each lane
+//      walks its targets' predecessor chains up to the first entry with
+//      known labels and unwinds them (hops + 1, rel * r: the reference's left
+//      fold, topology.c:1430, :1499, exactly), keeping every label it
+//      derives -- only the ~27% of entries on target paths (C4) are touched;
+//   4. tie export for rows whose target paths meet an ambiguous entry.
 #include <hip/hip_runtime.h>
 
 #include "pe_device.hpp"
@@ -40,8 +41,14 @@ namespace shdpe {
 
 constexpr int BT_THREADS = 1024;
 constexpr int BK = 4;        // arcs per vertex per load batch
-constexpr int BV = 2;        // vertices interleaved per group
-constexpr int LMAX = 4096;   // depth levels bucketed in LDS (deeper -> sweeps)
+// WPE = waves per SIMD the kernel is compiled for: 4 (128 VGPRs, one
+// 1024-thread workgroup per CU, two vertices interleaved per group) or 8
+// (64 VGPRs, two workgroups per CU, one vertex per group)
+template <int WPE> struct BCfg {
+    static constexpr int BV = WPE >= 8 ? 1 : 2;      // vertices interleaved per group
+    static constexpr int SMAX = WPE >= 8 ? 8 : 16;   // label-walk stack: (entry, arc) pairs per thread
+};
+constexpr int WALK_BUDGET = 2048;   // walk steps per target before the deep-tree sweeps
 
 struct alignas(16) BCtrl {
     int qtail;
@@ -55,37 +62,11 @@ struct alignas(16) BCtrl {
     unsigned long long busySum;
 };
 
-// Forward reliability fold with vertex factors (topology.c:1430-1462, :1499)
-// along lane l's predecessor chain, multiplied in source -> target order.
-// packed pointer-jumping entry: low word = ancestor J, high word = H
-__device__ __forceinline__ int jh_j(unsigned long long w) { return (int)(uint32_t)w; }
-__device__ __forceinline__ int jh_h(unsigned long long w) { return (int)(uint32_t)(w >> 32); }
-__device__ __forceinline__ void st_jh(unsigned long long* p, int j, int h) {
-    const unsigned long long w = (unsigned long long)(uint32_t)j | ((unsigned long long)(uint32_t)h << 32);
-    __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+__device__ __forceinline__ void st_wg(int32_t* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-
-// Wave-aggregated counter add: the lanes of a wave that bump the same
-// counter (depth levels: ~20 distinct keys for 10^6 entries) are merged into
-// one LDS atomic per distinct key instead of serialising 64 same-address
-// atomics.  Returns each participating lane's slot (old value + its rank).
-__device__ __forceinline__ int wave_agg_add(int* ctr, int key, bool act) {
-    unsigned long long pend = __ballot(act);
-    int pos = -1;
-    while (pend) {
-        const int leader = __ffsll((long long)pend) - 1;
-        const int k0 = __shfl(key, leader, 64);
-        const bool mine = act && key == k0 && ((pend >> __lane_id()) & 1ull);
-        const unsigned long long m = __ballot(mine);
-        int base = 0;
-        if ((int)__lane_id() == leader) base = atomicAdd(&ctr[k0], __popcll(m));
-        base = __shfl(base, leader, 64);
-        if (mine)
-            pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        pend &= ~m;
-    }
-    return pos;
+__device__ __forceinline__ void st_wg(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Forward reliability fold with vertex factors (topology.c:1430-1462, :1499)
@@ -103,11 +84,11 @@ __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
     for (int lo = 0; lo < h; lo += 64) {        // hops (lo, hi] counted from the source
         const int hi = min(h, lo + 64);
         int x = t;
-        for (int up = 0; up < h - hi; ++up) x = inCol[ld_wg(&P[(size_t)x * LB + l])];
+        for (int up = 0; up < h - hi; ++up) x = inCol[ld_wg(&P[(size_t)x * LB + l]) & ~TIE_AMB];
         double fac[64];
         int k = 0;
         while (k < hi - lo) {
-            const int a = ld_wg(&P[(size_t)x * LB + l]);
+            const int a = ld_wg(&P[(size_t)x * LB + l]) & ~TIE_AMB;
             fac[k++] = inRel[a];
             x = inCol[a];
         }
@@ -116,13 +97,16 @@ __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
     return acc;
 }
 
-template <int LB>
-__global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable tab0,
+template <int LB, int WPE>
+__global__ __launch_bounds__(BT_THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_batch_rows(DevGraph g0, DevTable tab0,
                                                            BatchScratch bs,
                                                            const int32_t* __restrict__ batchRows,
                                                            int32_t nBatches, uint8_t* rowAmbig,
                                                            double delta, int32_t* dbg,
                                                            const TieBuf* __restrict__ tieDesc) {
+    constexpr int BV = BCfg<WPE>::BV;
+    constexpr int SMAX = BCfg<WPE>::SMAX;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int tieSlot[LB];
     __shared__ unsigned long long tieThr[LB];
@@ -142,8 +126,6 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
     BCtrl* ctl = reinterpret_cast<BCtrl*>(smem);
     uint32_t* const any0 = reinterpret_cast<uint32_t*>(smem + 64);
     uint32_t* const any1 = any0 + nwp;
-    int32_t* const hist = reinterpret_cast<int32_t*>(any1 + nwp);   // [LMAX + 2]
-    int32_t* const cur = hist + (LMAX + 4);                           // [LMAX + 2]
 
     const size_t slot = blockIdx.x;
     const size_t NS = (size_t)bs.nStride;
@@ -152,12 +134,16 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
     double* R = as_global(bs.R + slot * SE);
     int32_t* H = as_global(bs.H + slot * SE);
     int32_t* P = as_global(bs.P + slot * SE);
-    int32_t* const X = as_global(bs.X + slot * 4 * SE);
-    unsigned long long* JH = reinterpret_cast<unsigned long long*>(X);   // 2 SE words
-    int2* LV = reinterpret_cast<int2*>(X + 2 * SE);                     // 2 SE words
     int32_t* Q = as_global(bs.queue + slot * NS);
 
-    for (int b = blockIdx.x; b < nBatches; b += gridDim.x) {
+    // batches are taken from a device counter (dynamic: a batch's cost varies
+    // by ~20%, and a workgroup finishing early takes the next one)
+    __shared__ int nextB;
+    for (;;) {
+        if (tid == 0) nextB = atomicAdd(bs.next, 1);
+        __syncthreads();
+        const int b = nextB;
+        if (b >= nBatches) break;
         const int row = batchRows[(size_t)b * LB + l];
         const int src = row >= 0 ? g.attached[row] : -1;
         // ---- init: dist = +inf for all (v, lane); pending sets empty ----
@@ -173,8 +159,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                 ctl->minNext = INF_BITS;
                 ctl->ambMask = 0u;
                 ctl->changed = 0;
-                ctl->maxDepth = 0;
-                ctl->busyMax = 0;
+                        ctl->busyMax = 0;
                 ctl->busySum = 0;
             }
         }
@@ -209,7 +194,6 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         const int phaseCap = 8 * n + 1024;
         long long procs = 0, arcsDone = 0, lanesAct = 0;
         double bound = delta;
-        uint32_t ambMask = 0u;
         for (;;) {   // phases + verification until the Bellman check holds
         for (;;) {
             uint32_t* const anyC = par ? any1 : any0;
@@ -372,9 +356,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         // (b) igraph sets parent[v] from the first POPPED tight predecessor:
         //     the tight in-arc with minimum dist[u]; equal minima from distinct
         //     vertices (or a zero-increment arc) -> the heap decides -> tie
-        //     row (k_exact_rows).  Also seeds the pointer jumping: J = parent
-        //     vertex (self for roots), depth 1 per tree arc.
-        bool amb = false;
+        //     row (k_exact_rows) if such an entry lies on a target's path.
         int viol = 0;
         {
             uint32_t* const anyC = par ? any1 : any0;
@@ -475,19 +457,21 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                     // the tie export below.
                     const bool ea = !root[v] && dvb[v] != INF_BITS &&
                                     (cnt[v] != 1 || best[v] == dvb[v]);
-                    amb |= ea;
-                    H[e] = ea ? 1 : 0;
-                    P[e] = tree ? ba[v] : -1;
-                    st_jh(&JH[e], tree ? bu[v] : vv, tree ? 1 : 0);
+                    // P: the tree IN-arc, TIE_AMB marking an entry whose
+                    // parent the heap decides; labels unresolved (-1) except
+                    // at the source (hops 0, rel 1: the fold's start)
+                    const int hx = tree ? ba[v] : -1;
+                    P[e] = ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx;
+                    const bool isSrc = vv == src;
+                    H[e] = isSrc ? 0 : -1;
+                    R[e] = isSrc ? 1.0 : -1.0;
                 }
             }
         }
-        if (amb) atomicOr(&ctl->ambMask, 1u << l);
         if (viol) ctl->changed = 1;
         fence_wg();
         __syncthreads();
         const int anyViol = ctl->changed;
-        ambMask = ctl->ambMask;
         __syncthreads();
         if (tid == 0) {
             ctl->changed = 0;
@@ -497,260 +481,36 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
         if (!anyViol || failed) break;
         ++repairs;
         }   // verification loop
-        // ---- tie export: rows whose parents the igraph heap decides go to
-        // k_exact_rows; hand it the final distances, these parents and the
-        // ambiguous entries, so it emulates the heap only until the last
-        // tied predecessor is popped (tie threshold) ----
-        if (ambMask && !failed && tieDesc) {
-            // descriptor read from memory here only: as a kernel argument
-            // it cost the hot loops registers (SGPR spills)
-            const TieBuf tie = *tieDesc;
-            if (tid < LB) {
-                int sl = -1;
-                if ((ambMask >> tid) & 1u) {
-                    sl = atomicAdd(tie.count, 1);
-                    if (sl >= tie.cap) sl = -1;
-                }
-                tieSlot[tid] = sl;
-                tieThr[tid] = 0ull;
-            }
-            __syncthreads();
-            const int sl = tieSlot[l];
-            unsigned long long thr = 0ull;
-            for (int v = gid; v < n; v += NG) {
-                if (sl < 0) continue;
-                const size_t e = (size_t)v * LB + l;
-                const int am = ld_wg(&H[e]);
-                const size_t o = (size_t)sl * (size_t)tie.n + v;
-                tie.D[o] = b2d(ld_wg(&D[e]));
-                const int pe = ld_wg(&P[e]);
-                tie.P[o] = am ? (TIE_AMB | (pe > 0 ? pe : 0)) : pe;
-                if (am) {   // rare: re-derive the tied (minimum tight) predecessor distance
-                    const unsigned long long dv = ld_wg(&D[e]);
-                    const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];
-                    const int a1 = undirected ? g.rowPtr[v + 1] : g.inPtr[v + 1];
-                    unsigned long long mt = INF_BITS;
-                    for (int a = a0; a < a1; ++a) {
-                        const int u = undirected ? g.col[a] : g.inCol[a];
-                        const double w = undirected ? g.lat[a] : g.inLat[a];
-                        const unsigned long long du = ld_wg(&D[(size_t)u * LB + l]);
-                        if (du <= dv && d2b(b2d(du) + w) == dv && du < mt) mt = du;
-                    }
-                    if (mt != INF_BITS) thr = mt > thr ? mt : thr;
-                }
-            }
-            if (thr) atomicMax(&tieThr[l], thr);
-            fence_wg();
-            __syncthreads();
-            if (gid == 0 && sl >= 0) tie.thr[sl] = b2d(tieThr[l]);
-        } else if (tid < LB) {
-            tieSlot[tid] = -1;
-        }
-        __syncthreads();
         const long long tPh2 = dbg ? (long long)clock64() : 0;
 
-        // ================= 3. hop counts: pointer jumping ====================
-        // JH[e] = (J, H) packed in one 8-B word: H = tree distance from v to
-        // its ancestor J; roots (and unreached entries) are (v, 0).  Jumping
-        // is in place: every read sees SOME consistent pair (single 8-B
-        // accesses), each a valid (ancestor, distance), so mixing old and new
-        // values only jumps further.  Entries that already point at a root
-        // are final and store ~H (negative): later rounds skip them without
-        // touching their parent, and children jump straight to the root.
-        int rounds = 0;
-        for (;;) {
-            int ch = 0, dmax = 0;
-            for (size_t e0 = (size_t)tid * 4; e0 < NE; e0 += (size_t)NT * 4) {
-                unsigned long long p[4], q[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const size_t e = e0 + k;
-                    p[k] = e < NE ? ld_wg(&JH[e]) : 0ull;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const size_t e = e0 + k;
-                    const int v = (int)(e / LB), ll = (int)(e % LB);
-                    const int j = jh_j(p[k]), h = jh_h(p[k]);
-                    const bool live = e < NE && j != v && h >= 0;
-                    q[k] = live ? ld_wg(&JH[(size_t)j * LB + ll]) : p[k];
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const size_t e = e0 + k;
-                    if (e >= NE) continue;
-                    const int v = (int)(e / LB);
-                    const int j = jh_j(p[k]), h = jh_h(p[k]);
-                    if (j == v) continue;                          // root / unreached
-                    if (h < 0) {                                   // final
-                        dmax = max(dmax, ~h);
-                        continue;
-                    }
-                    const int jj = jh_j(q[k]), hj = jh_h(q[k]);
-                    int nh;
-                    if (jj == j) nh = ~h;                          // parent is a root
-                    else if (hj < 0) nh = ~(h + ~hj);              // parent final
-                    else nh = h + hj;
-                    st_jh(&JH[e], jj, nh);
-                    ch = 1;
-                }
-            }
-            if (ch) ctl->changed = 1;
-            if (dmax) atomicMax(&ctl->maxDepth, dmax);
-            fence_wg();
-            __syncthreads();
-            const int any = ctl->changed;
-            __syncthreads();
-            if (tid == 0) ctl->changed = 0;
-            ++rounds;
-            if (!any) break;
-            if (tid == 0) ctl->maxDepth = 0;
-            __syncthreads();
-        }
-        const int maxDepth = ctl->maxDepth;
-        // unpack the hop counts into H (0 for roots / unreached) and, for the
-        // depth-ordered fold, histogram them
-        int32_t* const Hc = H;
-        if (maxDepth <= LMAX) {
-            for (int k = tid; k <= maxDepth + 1; k += NT) hist[k] = 0;
-            __syncthreads();
-        }
-        for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
-            int hh[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const size_t e = e0 + (size_t)k * NT;
-                hh[k] = e < NE ? jh_h(ld_wg(&JH[e])) : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const size_t e = e0 + (size_t)k * NT;
-                const int d = hh[k] < 0 ? ~hh[k] : 0;
-                if (e < NE) Hc[e] = d;
-                if (maxDepth <= LMAX) wave_agg_add(hist, d, e < NE && d > 0);
-            }
-        }
-        fence_wg();
-        __syncthreads();
-        const long long tPh3 = dbg ? (long long)clock64() : 0;
-
-        // ================= 4. reliability in depth order =====================
-        if (maxDepth <= LMAX) {
-            if (tid < 64) {
-                // exclusive scan of hist[1..maxDepth] by one wave
-                int carry = 0;
-                for (int base = 1; base <= maxDepth; base += 64) {
-                    const int k = base + tid;
-                    const int x = k <= maxDepth ? hist[k] : 0;
-                    int s = x;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const int y = __shfl_up(s, o, 64);
-                        if (tid >= o) s += y;
-                    }
-                    if (k <= maxDepth) { hist[k] = carry + s - x; cur[k] = carry + s - x; }
-                    carry += __shfl(s, 63, 64);
-                }
-                if (tid == 0) { hist[maxDepth + 1] = carry; cur[maxDepth + 1] = carry; }
-            }
-            __syncthreads();
-            // counting-sort scatter: LV[pos] = (entry, its tree in-arc)
-            for (size_t e0 = tid; e0 < NE; e0 += (size_t)NT * 4) {
-                int dd[4], aa[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const size_t e = e0 + (size_t)k * NT;
-                    dd[k] = e < NE ? ld_wg(&Hc[e]) : 0;
-                    aa[k] = e < NE ? ld_wg(&P[e]) : 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int pos = wave_agg_add(cur, dd[k], dd[k] > 0);
-                    if (pos >= 0) LV[pos] = make_int2((int)(e0 + (size_t)k * NT), aa[k]);
-                }
-            }
-            fence_wg();
-            __syncthreads();
-            // level by level; four entries per thread in flight (the level
-            // loop is a chain of dependent gathers, latency-bound otherwise)
-            for (int d = 1; d <= maxDepth; ++d) {
-                const int q0 = hist[d], q1 = hist[d + 1];
-                for (int qb = q0 + tid; qb < q1; qb += NT * 4) {
-                    int2 ea[4];
-                    int xs[4];
-                    double rr[4], rp[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int q = qb + k * NT;
-                        ea[k] = q < q1 ? LV[q] : make_int2(-1, 0);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int a = ea[k].x >= 0 ? ea[k].y : 0;
-                        xs[k] = g.inCol[a];
-                        rr[k] = g.inRel[a];
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int ll = (ea[k].x >= 0 ? ea[k].x : 0) % LB;
-                        rp[k] = ld_wg(&R[(size_t)xs[k] * LB + ll]);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (ea[k].x >= 0) R[ea[k].x] = rp[k] * rr[k];
-                }
-                fence_wg();
-                __syncthreads();
-            }
-        } else {
-            // very deep trees: Gauss-Seidel sweeps until nothing changes
-            for (;;) {
-                if (tid == 0) ctl->changed = 0;
-                __syncthreads();
-                int ch = 0;
-                for (size_t e = tid; e < NE; e += NT) {
-                    const int a = ld_wg(&P[e]);
-                    const int v = (int)(e / LB), ll = (int)(e % LB);
-                    if (a < 0 || v == src) continue;
-                    const int x = g.inCol[a];
-                    const double er = ld_wg(&R[(size_t)x * LB + ll]) * g.inRel[a];
-                    if (ld_wg(&R[e]) != er) { R[e] = er; ch = 1; }
-                }
-                if (ch) ctl->changed = 1;
-                fence_wg();
-                __syncthreads();
-                if (!ctl->changed) break;
-                __syncthreads();
-            }
-        }
-        const long long tPh4 = dbg ? (long long)clock64() : 0;
-        if (failed) ambMask = LBMASK;     // hand every row to k_exact_rows
-        // 0 fast path, 1 full igraph-heap emulation, 2 + slot: early-stop
-        // emulation with the exported tie data
-        if (gid == 0 && row >= 0)
-            rowAmbig[(size_t)b * LB + l] =
-                ((ambMask >> l) & 1u) ? (uint8_t)(tieSlot[l] >= 0 ? 2 + tieSlot[l] : 1) : (uint8_t)0;
-        if (dbg && tid == 0) {
-            dbg[16 * b + 0] = phases;
-            dbg[16 * b + 1] = rounds;
-            dbg[16 * b + 2] = maxDepth;
-            dbg[16 * b + 3] = (int)ambMask;
-            dbg[16 * b + 15] = repairs;
-            dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
-            dbg[16 * b + 6] = (int)((tPh2 - tPh1) >> 10);
-            dbg[16 * b + 7] = (int)((tPh3 - tPh2) >> 10);
-            dbg[16 * b + 11] = (int)((tPh4 - tPh3) >> 10);
-        }
-        if (dbg && l == 0 && procs) {
-            atomicAdd(&dbg[16 * b + 4], (int)procs);
-            atomicAdd(&dbg[16 * b + 9], (int)(arcsDone >> 4));
-            atomicAdd(&dbg[16 * b + 10], (int)lanesAct);
-        }
-
-        // ================= 5. row writer (topology.c:1805-1864) ==============
-        if (row >= 0 && !((ambMask >> l) & 1u)) {
+        // ================= 3. labels on demand + row writer ==================
+        // Only entries on some target's path need hops and reliability (27%
+        // of the entries at C4).  Each lane resolves a target by walking its
+        // predecessor chain up to the first entry with known labels (at the
+        // latest the source: hops 0, rel 1) and unwinding the walk:
+        // hops[x] = hops[p] + 1, rel[x] = rel[p] * r(p, x) -- the reference's
+        // left fold (topology.c:1430, :1499) in path order, exactly.  Unwound
+        // entries keep their labels for later walks of the same lane; each
+        // label is written once with the only value the fold can give, so a
+        // racing reader sees a complete pair (H >= 0 and R >= 0) or an
+        // unresolved entry and walks on.  The walk stack holds SMAX
+        // (entry, arc) pairs per thread in LDS (the relax bitmaps are dead);
+        // a longer chain is resolved from the top, SMAX levels at a time.
+        // An ambiguous entry (TIE_AMB) on a walked chain makes the row a tie
+        // row; ambiguous entries off every target path never matter.  Very
+        // deep trees (a walk over WALK_BUDGET steps: restarts cost
+        // O(depth^2 / SMAX)) switch to Gauss-Seidel sweeps over all entries
+        // and a second writer pass.
+        uint32_t relAmb = 0u;
+        for (int pass = 0; pass < 2; ++pass) {
+        bool deep = false;
+        if (!failed && row >= 0) {
+            int2* const stk = reinterpret_cast<int2*>(smem + 64);
             const int T = (int)tab.T;
             const size_t base = (size_t)(row - tab.rowStart) * (size_t)tab.T;
+            // pass 0: the deep-tree budget; pass 1: only the never-spin net
+            // (every consistent entry is resolved by then)
+            const long long stepCap = pass == 0 ? (long long)WALK_BUDGET : 4LL * n + 64;
             for (int j = gid; j < T; j += NG) {
                 const int t = g.attached[j];
                 double L = 0.0, Rl = 0.0;
@@ -773,11 +533,62 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                         f |= F_UNREACHABLE;
                     } else {
                         L = b2d(dt);
-                        h = ld_wg(&Hc[e]);
+                        int he = ld_wg(&H[e]);
+                        double re = ld_wg(&R[e]);
+                        long long steps = 0;
+                        int cur = (int)e;
+                        while (!(he >= 0 && re >= 0.0)) {
+                            int sp = 0, x = cur, hp = 0;
+                            double rp = 0.0;
+                            bool found = false;
+                            while (sp < SMAX) {
+                                const int a = ld_wg(&P[x]);
+                                if (a < 0 || ++steps > stepCap) {
+                                    if (a >= 0 && pass == 0) deep = true;   // -> sweeps
+                                    else relAmb = 1u;      // no parent / a cycle: exact path
+                                    sp = 0;
+                                    found = true;
+                                    break;
+                                }
+                                relAmb |= (uint32_t)((a & TIE_AMB) != 0);
+                                const int arc = a & ~TIE_AMB;
+                                stk[sp * NT + tid] = make_int2(x, arc);
+                                ++sp;
+                                const int pe = g.inCol[arc] * LB + l;
+                                const int hq = ld_wg(&H[pe]);
+                                const double rq = ld_wg(&R[pe]);
+                                if (hq >= 0 && rq >= 0.0) {
+                                    hp = hq;
+                                    rp = rq;
+                                    found = true;
+                                    break;
+                                }
+                                x = pe;
+                            }
+                            if (!found) {           // chain longer than SMAX: its top first
+                                cur = x;
+                                continue;
+                            }
+                            for (int i = sp - 1; i >= 0; --i) {
+                                const int2 sx = stk[i * NT + tid];
+                                hp += 1;
+                                rp = rp * g.inRel[sx.y];
+                                st_wg(&H[sx.x], hp);
+                                st_wg(&R[sx.x], rp);
+                            }
+                            if (sp == 0) break;     // gave up (deep / inconsistent)
+                            if (cur == (int)e) {
+                                he = hp;
+                                re = rp;
+                                break;
+                            }
+                            cur = (int)e;           // top segment resolved: walk again
+                        }
+                        h = he;
                         const int pa = ld_wg(&P[e]);
-                        pv = pa >= 0 ? g.inCol[pa] : -1;
+                        pv = pa >= 0 ? g.inCol[pa & ~TIE_AMB] : -1;
                         if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
-                            Rl = ld_wg(&R[e]);
+                            Rl = re;
                         else
                             Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
                         if (L == 0.0) {                 // topology.c:1848-1852
@@ -793,32 +604,173 @@ __global__ __launch_bounds__(BT_THREADS) void k_batch_rows(DevGraph g0, DevTable
                 if (tab.pred) tab.pred[base + j] = pv;
             }
         }
+        if (deep) ctl->changed = 1;
+        fence_wg();
+        __syncthreads();
+        const int anyDeep = ctl->changed;
+        __syncthreads();
+        if (tid == 0) ctl->changed = 0;
+        __syncthreads();
+        if (!anyDeep) break;
+        // Gauss-Seidel: every tree entry whose parent has labels takes them
+        // (+1, * r) until a sweep changes nothing (<= depth sweeps).  These
+        // entries were not walked, so an ambiguous one sends its row to the
+        // exact path (conservative).  Cycles of zero-increment parents stay
+        // unresolved and the second pass's walks flag them.
+        for (int sweep = 0; sweep <= n + 1; ++sweep) {
+            int ch = 0;
+            for (size_t e = tid; e < NE; e += NT) {
+                const int a = ld_wg(&P[e]);
+                if (a < 0) continue;
+                const int ll = (int)(e % LB);
+                const int arc = a & ~TIE_AMB;
+                const int pe = g.inCol[arc] * LB + ll;
+                const int hq = ld_wg(&H[pe]);
+                const double rq = ld_wg(&R[pe]);
+                if (hq < 0 || rq < 0.0) continue;
+                const int hn = hq + 1;
+                const double rn = rq * g.inRel[arc];
+                if (ld_wg(&H[e]) != hn || ld_wg(&R[e]) != rn) {
+                    st_wg(&H[e], hn);
+                    st_wg(&R[e], rn);
+                    ch = 1;
+                    if (a & TIE_AMB) atomicOr(&ctl->ambMask, 1u << ll);
+                }
+            }
+            if (ch) ctl->changed = 1;
+            fence_wg();
+            __syncthreads();
+            const int any = ctl->changed;
+            __syncthreads();
+            if (tid == 0) ctl->changed = 0;
+            __syncthreads();
+            if (!any) break;
+        }
+        }   // writer passes
+        if (relAmb) atomicOr(&ctl->ambMask, 1u << l);
+        fence_wg();
+        __syncthreads();
+        // rows whose target paths meet an ambiguous entry (or that hit the
+        // phase cap) go to k_exact_rows; their rows above are rewritten there
+        const uint32_t needMask = failed ? LBMASK : ctl->ambMask;
+        __syncthreads();
+        if (tid == 0) ctl->ambMask = 0u;
+        const long long tPh3 = dbg ? (long long)clock64() : 0;
+
+        // ---- tie export: hand k_exact_rows the final distances, the parents
+        // and the ambiguous entries, so it emulates the heap only until the
+        // last tied predecessor is popped (tie threshold) ----
+        if (needMask && !failed && tieDesc) {
+            // descriptor read from memory here only: as a kernel argument
+            // it cost the hot loops registers (SGPR spills)
+            const TieBuf tie = *tieDesc;
+            if (tid < LB) {
+                int sl = -1;
+                if ((needMask >> tid) & 1u) {
+                    sl = atomicAdd(tie.count, 1);
+                    if (sl >= tie.cap) sl = -1;
+                }
+                tieSlot[tid] = sl;
+                tieThr[tid] = 0ull;
+            }
+            __syncthreads();
+            const int sl = tieSlot[l];
+            unsigned long long thr = 0ull;
+            for (int v = gid; v < n; v += NG) {
+                if (sl < 0) continue;
+                const size_t e = (size_t)v * LB + l;
+                const int pe = ld_wg(&P[e]);
+                const bool am = pe >= 0 && (pe & TIE_AMB);
+                const size_t o = (size_t)sl * (size_t)tie.n + v;
+                tie.D[o] = b2d(ld_wg(&D[e]));
+                tie.P[o] = pe;
+                if (am) {   // rare: re-derive the tied (minimum tight) predecessor distance
+                    const unsigned long long dv = ld_wg(&D[e]);
+                    const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];
+                    const int a1 = undirected ? g.rowPtr[v + 1] : g.inPtr[v + 1];
+                    unsigned long long mt = INF_BITS;
+                    for (int a = a0; a < a1; ++a) {
+                        const int u = undirected ? g.col[a] : g.inCol[a];
+                        const double w = undirected ? g.lat[a] : g.inLat[a];
+                        const unsigned long long du = ld_wg(&D[(size_t)u * LB + l]);
+                        if (du <= dv && d2b(b2d(du) + w) == dv && du < mt) mt = du;
+                    }
+                    if (mt != INF_BITS) thr = mt > thr ? mt : thr;
+                }
+            }
+            if (thr) atomicMax(&tieThr[l], thr);
+            fence_wg();
+            __syncthreads();
+            if (gid == 0 && sl >= 0) tie.thr[sl] = b2d(tieThr[l]);
+        } else if (tid < LB) {
+            tieSlot[tid] = -1;
+        }
+        __syncthreads();
+        const long long tPh4 = dbg ? (long long)clock64() : 0;
+        // 0 fast path, 1 full igraph-heap emulation, 2 + slot: early-stop
+        // emulation with the exported tie data
+        if (gid == 0 && row >= 0)
+            rowAmbig[(size_t)b * LB + l] =
+                ((needMask >> l) & 1u) ? (uint8_t)(tieSlot[l] >= 0 ? 2 + tieSlot[l] : 1) : (uint8_t)0;
+        if (dbg && tid == 0) {
+            dbg[16 * b + 0] = phases;
+            dbg[16 * b + 1] = 0;
+            dbg[16 * b + 2] = 0;
+            dbg[16 * b + 3] = (int)needMask;
+            dbg[16 * b + 15] = repairs;
+            dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
+            dbg[16 * b + 6] = (int)((tPh2 - tPh1) >> 10);
+            dbg[16 * b + 7] = (int)((tPh3 - tPh2) >> 10);
+            dbg[16 * b + 11] = (int)((tPh4 - tPh3) >> 10);
+        }
+        if (dbg && l == 0 && procs) {
+            atomicAdd(&dbg[16 * b + 4], (int)procs);
+            atomicAdd(&dbg[16 * b + 9], (int)(arcsDone >> 4));
+            atomicAdd(&dbg[16 * b + 10], (int)lanesAct);
+        }
         fence_wg();
         __syncthreads();
         if (dbg && tid == 0) dbg[16 * b + 8] = (int)(((long long)clock64() - tPh4) >> 10);
     }
 }
 
-template <int LB>
+template <int LB, int WPE>
 static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st,
                       int grid) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB, WPE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-    hipLaunchKernelGGL(k_batch_rows<LB>, dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
+    hipLaunchKernelGGL((k_batch_rows<LB, WPE>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
                        bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
 }
 
-int batch_lds_bytes(int n) {
+int batch_lds_bytes(int n, int wpe) {
     const int nwp = (((n + 31) >> 5) + 3) & ~3;
-    return 64 + 2 * 4 * nwp + 2 * 4 * (LMAX + 4);
+    // label walks reuse the relax bitmaps' LDS for their stacks
+    const int stack = BT_THREADS * (wpe >= 8 ? BCfg<8>::SMAX : BCfg<4>::SMAX) * 8;
+    return 64 + (2 * 4 * nwp > stack ? 2 * 4 * nwp : stack);
 }
 
-const void* batch_kernel_ptr(int lb) {
-    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8>);
-    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32>);
-    return reinterpret_cast<const void*>(&k_batch_rows<16>);
+template <int WPE>
+static const void* kptr(int lb) {
+    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8, WPE>);
+    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32, WPE>);
+    return reinterpret_cast<const void*>(&k_batch_rows<16, WPE>);
+}
+
+const void* batch_kernel_ptr(int lb, int wpe) { return wpe >= 8 ? kptr<8>(lb) : kptr<4>(lb); }
+
+template <int WPE>
+static void launch_w(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
+                     const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
+                     const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid) {
+    if (cfg.lb == 8)
+        launch_lb<8, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    else if (cfg.lb == 32)
+        launch_lb<32, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    else
+        launch_lb<16, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
 }
 
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
@@ -827,12 +779,10 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
     if (nBatches <= 0) return;
     const int grid = nBatches < cfg.grid ? nBatches : cfg.grid;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (cfg.lb == 8)
-        launch_lb<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
-    else if (cfg.lb == 32)
-        launch_lb<32>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    if (cfg.wpe >= 8)
+        launch_w<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else
-        launch_lb<16>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_w<4>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
 }
 
 }  // namespace shdpe

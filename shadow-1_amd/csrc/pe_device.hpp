@@ -74,7 +74,7 @@ struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0;
-    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 0;
+    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 0, batchWpe = 0;
     double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
@@ -100,11 +100,11 @@ struct DevScratch {
 // access).
 struct BatchScratch {
     unsigned long long* D;   // [slot][nStride][LB] f64 bit patterns (dist)
-    double* R;               // [slot][nStride][LB] rel product label
-    int32_t* H;              // [slot][nStride][LB] hop label
-    int32_t* P;              // [slot][nStride][LB] chosen IN-arc, -1 none
-    int32_t* X;              // [slot][4][nStride*LB] pointer-jumping / level lists
+    double* R;               // [slot][nStride][LB] rel product label (< 0 unresolved)
+    int32_t* H;              // [slot][nStride][LB] hop label (-1 unresolved)
+    int32_t* P;              // [slot][nStride][LB] chosen IN-arc (| TIE_AMB), -1 none
     int32_t* queue;          // [slot][nStride] phase candidate list
+    int32_t* next;           // next batch to take (device counter, zeroed per launch)
     int64_t nStride;         // >= n, multiple of 64
 };
 
@@ -113,6 +113,7 @@ struct BatchLaunch {
     int32_t threads;         // workgroup size
     int32_t grid;            // resident workgroups (= scratch slots)
     int32_t ldsBytes;
+    int32_t wpe;             // waves per SIMD the kernel variant is built for (4 or 8)
     double delta;            // bucket width
 };
 
@@ -189,8 +190,8 @@ int sparse_max_threads();
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream);
-const void* batch_kernel_ptr(int lb);
-int batch_lds_bytes(int n);
+const void* batch_kernel_ptr(int lb, int wpe);
+int batch_lds_bytes(int n, int wpe);
 // batched helpers (pe_aux.hip), all on `stream`
 void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, int64_t nEdges,
                        double* dLat, double* dRel, uint8_t* dFlags, void* stream);

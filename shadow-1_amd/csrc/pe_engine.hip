@@ -149,6 +149,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_THREADS", t.batchThreads);
     gi("SHDPE_BATCH_GRID", t.batchGrid);
     gi("SHDPE_BATCH_ORDER", t.batchOrder);
+    gi("SHDPE_BATCH_WPE", t.batchWpe);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -266,17 +267,25 @@ static int configure(ShdPe* pe, Shard* sh) {
         b.lb = ((int64_t)sh->rowCount + 15) / 16 < (int64_t)sh->numCUs ? 8 : 16;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
-    b.ldsBytes = batch_lds_bytes((int)n);
+    // kernel variant: 8 waves per SIMD (two workgroups per CU) when two fit
+    // the CU's LDS, else 4 (SHDPE_BATCH_WPE forces one)
+    auto occupancy = [&](int wpe) {
+        const int lds = batch_lds_bytes((int)n, wpe);
+        int per = 0;
+        if (lds > LDS ||
+            hipFuncSetAttribute(batch_kernel_ptr(b.lb, wpe), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, batch_kernel_ptr(b.lb, wpe), b.threads,
+                                                         lds) != hipSuccess)
+            per = 0;
+        return per;
+    };
+    b.wpe = tu.batchWpe == 4 || tu.batchWpe == 8 ? tu.batchWpe : (occupancy(8) >= 2 ? 8 : 4);
+    b.ldsBytes = batch_lds_bytes((int)n, b.wpe);
     if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
-    int bPerCU = 1;
-    if (b.ldsBytes <= LDS &&
-        (hipFuncSetAttribute(batch_kernel_ptr(b.lb), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             b.ldsBytes) != hipSuccess ||
-         hipOccupancyMaxActiveBlocksPerMultiprocessor(&bPerCU, batch_kernel_ptr(b.lb), b.threads,
-                                                      b.ldsBytes) != hipSuccess ||
-         bPerCU < 1))
-        bPerCU = 1;
+    int bPerCU = b.ldsBytes <= LDS ? occupancy(b.wpe) : 1;
+    if (bPerCU < 1) bPerCU = 1;
     b.grid = sh->numCUs * bPerCU;
     if (tu.batchGrid > 0 && tu.batchGrid < b.grid) b.grid = tu.batchGrid;
     b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
@@ -649,7 +658,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     if (sh->batchReady) return SHD_PE_OK;
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     const size_t LB = (size_t)sh->bcfg.lb;
-    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4 + 16) + NS * 4;
+    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4) + NS * 4;
     // scratch budget (default 64 GiB): fewer resident batches on huge graphs
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
@@ -657,11 +666,10 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const size_t slots = std::min<size_t>({(size_t)sh->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
     sh->bcfg.grid = (int32_t)slots;
     int rc;
-    void *D, *R, *H, *P, *X, *q, *rows, *amb;
+    void *D, *R, *H, *P, *q, *rows, *amb;
     if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
-        (rc = dev_alloc(sh, &X, slots * NS * LB * 16)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
-        (rc = dev_alloc(sh, &q, slots * NS * 4)) ||
+        (rc = dev_alloc(sh, &q, slots * NS * 4 + 64)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
         (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)))
         return rc;
@@ -669,8 +677,8 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.R = (double*)R;
     sh->bsc.H = (int32_t*)H;
     sh->bsc.P = (int32_t*)P;
-    sh->bsc.X = (int32_t*)X;
     sh->bsc.queue = (int32_t*)q;
+    sh->bsc.next = (int32_t*)q + slots * NS;
     sh->bsc.nStride = (int64_t)NS;
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
@@ -716,11 +724,11 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
 // re-visits, jump rounds, per-batch cost spread.
 static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t nB) {
     double ph = 0, pr = 0, kc[5] = {0, 0, 0, 0, 0}, arcsP = 0, lanesP = 0, bmax = 0, bmean = 0, cand = 0;
-    long rnd = 0, dmax = 0, ambB = 0, rep = 0;
+    long ambB = 0, rep = 0;
     double tMin = 1e30, tMax = 0, tSum = 0, tSq = 0;
     for (int32_t i = 0; i < nB; ++i) {
         const int32_t* d = d0 + 16 * i;
-        ph += d[0]; rnd += d[1]; dmax = std::max<long>(dmax, d[2]);
+        ph += d[0];
         ambB += d[3] != 0;
         rep += d[15];
         pr += d[4];
@@ -739,13 +747,13 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
                  sh->gindex, bmax / nB / 1e6, bmean / nB / 1e6, cand / nB);
     std::fprintf(stderr, "[shdpe] batch arc-visits/batch=%.0f (%.2f x nArcs) active lanes/proc=%.2f\n",
                  arcsP / nB, arcsP / nB / (double)pe->hg.nArcs(), lanesP / std::max(pr, 1.0));
-    std::fprintf(stderr, "[shdpe] batch Mcycles/batch: relax=%.2f pred=%.2f depth=%.2f rel=%.2f write=%.2f | "
+    std::fprintf(stderr, "[shdpe] batch Mcycles/batch: relax=%.2f pred=%.2f labels+write=%.2f tie-export=%.2f tail=%.2f | "
                  "per-batch total min=%.2f mean=%.2f max=%.2f sd=%.2f\n", kc[0] / nB / 1e6, kc[1] / nB / 1e6,
                  kc[2] / nB / 1e6, kc[3] / nB / 1e6, kc[4] / nB / 1e6, tMin / 1e6, mean / 1e6, tMax / 1e6, sd / 1e6);
     std::fprintf(stderr, "[shdpe] batch LB=%d batches=%d grid=%d delta=%.3f | phases/batch=%.1f "
-                 "vertex-procs/batch=%.0f (%.2f per vertex) | jump rounds/batch=%.1f max depth=%ld amb batches=%ld repairs=%ld\n",
+                 "vertex-procs/batch=%.0f (%.2f per vertex) | tie batches=%ld repairs=%ld\n",
                  sh->bcfg.lb, nB, sh->bcfg.grid, sh->bcfg.delta, ph / nB, pr / nB,
-                 pr / nB / pe->hg.n, (double)rnd / nB, dmax, ambB, rep);
+                 pr / nB / pe->hg.n, ambB, rep);
 }
 
 static void print_sparse_debug(ShdPe* pe, Shard* sh, const int32_t* dbg, int32_t cnt) {
@@ -849,6 +857,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                                   hipMemcpyHostToDevice, sh->stream));
             if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 64, sh->stream));
             if (sh->tie.cap > 0) HIPCHK(hipMemsetAsync(sh->tie.count, 0, 4, sh->stream));
+            HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
                               sh->dDbg, sh->dTie, sh->stream);

@@ -486,11 +486,11 @@ def test_topology_shim_concurrent_readers(E, oracle_mod):
     eng.close()
 
 
-@pytest.mark.parametrize("n,ok", [(520_000, True), (530_000, False)])
+@pytest.mark.parametrize("n,ok", [(650_000, True), (660_000, False)])
 def test_vertex_limit_of_batched_kernel(E, oracle_mod, n, ok):
-    """k_batch_rows keeps two pending bitmaps + the depth histogram in LDS:
-    about 523.9k vertices fit 160 KB.  Past that, shd_pe_create refuses the
-    graph with SHD_PE_ETOOBIG instead of failing every later launch."""
+    """k_batch_rows keeps two pending bitmaps in LDS: up to 655,104 vertices
+    fit 160 KB.  Past that, shd_pe_create refuses the graph with
+    SHD_PE_ETOOBIG instead of failing every later launch."""
     rng = np.random.default_rng(n)
     perm = rng.permutation(n)
     extra = rng.integers(0, n, size=(n, 2))
