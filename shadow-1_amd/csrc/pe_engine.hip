@@ -268,7 +268,7 @@ static int configure(ShdPe* pe, Shard* sh) {
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     // kernel variant: 8 waves per SIMD (two workgroups per CU) when two fit
-    // the CU's LDS, else 4 (SHDPE_BATCH_WPE forces one)
+    // the CU's LDS, else 4 (SHDPE_BATCH_WPE forces one) ...
     auto occupancy = [&](int wpe) {
         const int lds = batch_lds_bytes((int)n, wpe);
         int per = 0;
@@ -280,7 +280,12 @@ static int configure(ShdPe* pe, Shard* sh) {
             per = 0;
         return per;
     };
-    b.wpe = tu.batchWpe == 4 || tu.batchWpe == 8 ? tu.batchWpe : (occupancy(8) >= 2 ? 8 : 4);
+    // (and only when the shard has a batch for every one of those workgroups:
+    // C4 per-rank shard times N = 4 / 8, profiles/r02l_shard_times.txt)
+    const int64_t nBatchesAll = ((int64_t)sh->rowCount + b.lb - 1) / b.lb;
+    b.wpe = tu.batchWpe == 4 || tu.batchWpe == 8
+                ? tu.batchWpe
+                : (nBatchesAll >= 2LL * sh->numCUs && occupancy(8) >= 2 ? 8 : 4);
     b.ldsBytes = batch_lds_bytes((int)n, b.wpe);
     if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;

@@ -5,12 +5,13 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(R, "shadow-1_amd")]
 import numpy as np
 from shdpe import generators as G
-from shdpe.engine import Engine
+from shdpe.engine import Engine, DEBUG_ENV
 
 wl = sys.argv[1]
 top, att = G.make_config(wl)
 for N in [int(x) for x in sys.argv[2:]]:
-    eng = Engine(top, att, shard_index=0, shard_count=N)
+    dbg = DEBUG_ENV if any(k.startswith("SHDPE_") for k in os.environ) else 0
+    eng = Engine(top, att, shard_index=0, shard_count=N, debug_flags=dbg)
     s0, cnt = eng.owned
     pos = np.arange(s0, s0 + cnt, dtype=np.int32)
     eng.compute_positions(s0, cnt)           # warm-up (allocations)
@@ -23,5 +24,6 @@ for N in [int(x) for x in sys.argv[2:]]:
         best = min(best, time.perf_counter() - t)
     st = eng.stats()
     print(f"{wl} N={N} rows={cnt} ms={best*1e3:.1f} lanes={st['batchLanes']} "
-          f"rows/s/gpu={cnt/best:.0f} -> {N*cnt/best:.0f} total", flush=True)
+          f"rows/s/gpu={cnt/best:.0f} -> {N*cnt/best:.0f} total "
+          f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('SHDPE_'))}]", flush=True)
     eng.close()
