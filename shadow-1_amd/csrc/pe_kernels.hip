@@ -702,8 +702,14 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
     #pragma unroll
                     for (int k = 0; k < UNR; ++k) {       // branch-free (see process_group)
                         const int ac = a + k < a1 ? a + k : a;
-                        cu[k] = g.inCol[ac];
-                        lw[k] = g.inLat[ac];
+                        if (undirected) {   // the relax loop's 12-B arcs: one L2 copy of the graph
+                            const Arc3 A = g.arc3[ac];
+                            cu[k] = A.col;
+                            lw[k] = __hiloint2double((int)A.latHi, (int)A.latLo);
+                        } else {
+                            cu[k] = g.inCol[ac];
+                            lw[k] = g.inLat[ac];
+                        }
                     }
     #pragma unroll
                     for (int k = 0; k < UNR; ++k) du[k] = c.dist[cu[k]];

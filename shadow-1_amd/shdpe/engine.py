@@ -79,10 +79,12 @@ _lib = None
 
 
 def load_library(path: str = LIB_PATH):
-    """Load libshdpe.so; raises if it has not been built (no fallback)."""
+    """Load libshdpe.so; raises if it has not been built (no fallback).
+    SHDPE_LIB names another build of the same library (same-box A/B runs)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("SHDPE_LIB") or path
     if not os.path.exists(path):
         raise RuntimeError(f"libshdpe.so not built at {path}: run "
                            "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C shadow-1_amd)")
