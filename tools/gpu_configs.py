@@ -4,12 +4,12 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(R, "shadow-1_amd"), os.path.join(R, "oracle")]
 import numpy as np
 from shdpe import generators as G
-from shdpe.engine import Engine
+from shdpe.engine import Engine, DEBUG_ENV
 from oracle import OracleGraph
 
 for wl in sys.argv[1].split(","):
     t0 = time.time(); top, att = G.make_config(wl); tg = time.time() - t0
-    eng = Engine(top, att)
+    eng = Engine(top, att, debug_flags=DEBUG_ENV if any(k.startswith('SHDPE_') for k in os.environ) else 0)
     st0 = eng.stats()
     nrows = int(os.environ.get("QROWS", "2048"))
     nrows = min(nrows, eng.T)
@@ -21,7 +21,7 @@ for wl in sys.argv[1].split(","):
           f"rows/s={nrows/(st['msTotal']/1e3):.0f} -> full table est {eng.T/(nrows/(st['msTotal']/1e3)):.2f}s", flush=True)
     og = OracleGraph(top)
     rng = np.random.default_rng(0)
-    srcs = eng.attached[rng.choice(nrows, 6, replace=False)]
+    srcs = eng.attached[rng.choice(nrows, int(os.environ.get('PROWS', '6')), replace=False)]
     bad = 0
     t0 = time.time()
     exp = og.rows(srcs, eng.attached, threads=8)
