@@ -8,6 +8,7 @@ of complete graphs).  Bar: lat / rel bit-exact, hops / pred / flags identical
 top where the oracle cannot cover every row.
 """
 import os
+import sys
 import threading
 
 import numpy as np
@@ -345,3 +346,71 @@ def test_get_row_from_8_threads(E):
         t.join()
     assert not errors, errors[:5]
     eng.close()
+
+
+_RANK_SCRIPT = r"""
+import os, sys
+import numpy as np
+root = sys.argv[1]
+sys.path[:0] = [os.path.join(root, "shadow-1_amd")]
+import torch
+import torch.distributed as dist
+from shdpe import generators as G
+from shdpe.engine import Engine
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+top = G.power_law(20_000, m=3, seed=41)
+att = G.sample_attached(top.n, 1000, seed=3)
+eng = Engine(top, att, device=0, force_mode=5, shard_index=rank, shard_count=world)
+eng.compute_all()
+s0, cnt = eng.owned
+rows = eng.get_rows(s0, cnt)
+T = eng.T
+out = {}
+for k in ("lat", "rel", "hops", "pred", "flags"):
+    blk = torch.from_numpy(np.ascontiguousarray(rows[k]).view(np.uint8).reshape(-1).copy())
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([blk.numel()], dtype=torch.int64))
+    mx = int(max(s.item() for s in sizes))
+    pad = torch.zeros(mx, dtype=torch.uint8)
+    pad[:blk.numel()] = blk
+    parts = [torch.zeros(mx, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    out[k] = np.concatenate([p[:int(s.item())].numpy() for p, s in zip(parts, sizes)])
+if rank == 0:
+    np.savez(sys.argv[2], **out)
+dist.barrier()
+eng.close()
+dist.destroy_process_group()
+"""
+
+
+def test_two_rank_processes_gloo_gather_match_single_engine(E, tmp_path):
+    """Two rank processes on the test GPU (what bench.py --gpus 2 runs, one
+    engine per rank with shardIndex / shardCount), their row blocks exchanged
+    over gloo (all fields): the assembled table is byte-identical to one
+    engine's.  The ranks share one GPU here, so the exchange cannot be RCCL
+    (one device per rank); the engine-owned RCCL gather is covered by the
+    in-process multi-shard tests above."""
+    import socket
+    import subprocess
+    top, att, force = _shard_case("batched")
+    one = E.Engine(top, att, force_mode=force)
+    one.compute_all()
+    ref = _all_rows(one)
+    one.close()
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    out = str(tmp_path / "table.npz")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", _RANK_SCRIPT, root, out], env=env))
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    got = np.load(out)
+    for k in FIELDS:
+        assert np.array_equal(got[k], ref[k].view(np.uint8).reshape(-1)), k
