@@ -512,3 +512,37 @@ def test_vertex_limit_of_batched_kernel(E, oracle_mod, n, ok):
         with pytest.raises(E.EngineError) as ei:
             E.Engine(top, att)
         assert ei.value.code == E.ETOOBIG
+
+
+def _twin_tie_graph(z_attached, seed=11):
+    """A tie-free random graph plus twins a, b (both hanging off hub h with
+    the same latency) and z adjacent to exactly a and b with equal latency:
+    for every other source z has two equal-minimum tight predecessors (the
+    heap decides its parent), and z is a leaf."""
+    base = G.random_sparse(600, 5, seed=seed)
+    n0 = base.n
+    a, b, z, h = n0, n0 + 1, n0 + 2, 0
+    src = np.concatenate([base.src, [h, h, a, b, a, b, z]])
+    dst = np.concatenate([base.dst, [a, b, z, z, a, b, z]])
+    lat = np.concatenate([base.latency, [7.25, 7.25, 3.5, 3.5, 1.0, 1.0, 1.0]])
+    loss = np.concatenate([base.loss, [0.01, 0.01, 0.0, 0.0, 0.0, 0.0, 0.0]])
+    top = Topology(n0 + 3, False, src, dst, lat, loss, None)
+    att = np.arange(0, n0, 3, dtype=np.int32)
+    if z_attached:
+        att = np.concatenate([att, [z]]).astype(np.int32)
+    return top, att
+
+
+@pytest.mark.parametrize("z_attached", [False, True])
+def test_batched_tie_relevance(E, oracle_mod, z_attached):
+    """k_batch_rows sends a row to the exact path only when an ambiguous
+    entry lies on a target's path: with z (ambiguous in every row but a's,
+    b's and z's own) off every target path all rows stay on the fast path;
+    with z a target every row is a tie row.  Bit-exact either way."""
+    top, att = _twin_tie_graph(z_attached)
+    st = _check_engine(E, oracle_mod, top, att, force=5)
+    assert st["batched"] == 1
+    if z_attached:
+        assert st["rowsExact"] >= len(att) - 1
+    else:
+        assert st["rowsExact"] == 0
