@@ -213,6 +213,11 @@ def main():
         kname = "k_batch_rows" if st["batched"] else "k_sparse_rows"
         achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
+    traffic_bytes = (traffic or {}).get("bytes_per_launch")
+    if traffic_bytes and count != T:
+        # the PMC capture is of the whole table on one GPU; a shard's launch
+        # moves its share (per-row traffic is uniform across batches)
+        traffic_bytes = traffic_bytes * count / T
     out = {
         "metric": "path-table source rows/sec (latency+reliability)",
         "value": value,
@@ -233,7 +238,7 @@ def main():
         "edges_relaxed_per_s": m_arcs * rows_total / elapsed,
         "roofline": {"bound": bound, "kernel": kname, "achieved": achieved,
                      "peak": peak, "unit": unit, "frac": achieved / peak,
-                     "traffic": (traffic or {}).get("bytes_per_launch"),
+                     "traffic": traffic_bytes,
                      "algorithmic_per_launch": bytes_per_launch,
                      "avg_launch_ms": avg_launch_ms, "launches": launches},
         "rows_exact": st["rowsExact"] // max(1, args.steps),
@@ -246,7 +251,7 @@ def main():
         if bound == "hbm":
             out["roofline"]["frac_of_stream"] = achieved / sbw
             tb = out["roofline"]["traffic"]
-            if tb and world == 1:
+            if tb:
                 # measured L2-miss bytes (PMC, profiles/traffic_<wl>.json) over
                 # this run's launch time: how close the kernel runs to the
                 # bandwidth it actually moves
