@@ -56,7 +56,7 @@ struct alignas(16) BCtrl {
     unsigned long long minNext;
     unsigned int ambMask;
     int changed;
-    int maxDepth;
+    int htail;        // heavy-vertex list (grows down from the top of the queue)
     int pad;
     unsigned long long busyMax;
     unsigned long long busySum;
@@ -159,6 +159,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->minNext = INF_BITS;
                 ctl->ambMask = 0u;
                 ctl->changed = 0;
+                ctl->htail = 0;
                         ctl->busyMax = 0;
                 ctl->busySum = 0;
             }
@@ -199,22 +200,38 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             uint32_t* const anyC = par ? any1 : any0;
             uint32_t* const anyN = par ? any0 : any1;
             // candidates = vertices with a pending bit (cur set, consumed)
+            // (hubs -- degree >= the engine's heavy threshold -- go to a list
+            // of their own, processed by whole waves: one 16-lane group on a
+            // hub's ~1000 arcs would set the phase's length)
             for (int w = tid; w < nw; w += NT) {
                 uint32_t bits = anyC[w];
                 if (bits) {
                     anyC[w] = 0u;
-                    int pos = atomicAdd(&ctl->qtail, __popc(bits));
-                    while (bits) {
-                        const int bb = __ffs(bits) - 1;
-                        bits &= bits - 1;
-                        Q[pos++] = (w << 5) + bb;
+                    uint32_t hv = bits & g.heavyBits[w];
+                    bits &= ~hv;
+                    if (bits) {
+                        int pos = atomicAdd(&ctl->qtail, __popc(bits));
+                        while (bits) {
+                            const int bb = __ffs(bits) - 1;
+                            bits &= bits - 1;
+                            Q[pos++] = (w << 5) + bb;
+                        }
+                    }
+                    if (hv) {
+                        int pos = atomicAdd(&ctl->htail, __popc(hv));
+                        while (hv) {
+                            const int bb = __ffs(hv) - 1;
+                            hv &= hv - 1;
+                            Q[NS - 1 - pos++] = (w << 5) + bb;
+                        }
                     }
                 }
             }
             fence_wg();
             __syncthreads();
             const int qn = ctl->qtail;
-            if (qn == 0) break;
+            const int hn = ctl->htail;
+            if (qn == 0 && hn == 0) break;
             if (phases > phaseCap) {        // safety net: never spin the GPU
                 failed = true;
                 break;
@@ -229,7 +246,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
             for (int v = 0; v < BV; ++v) {
                 const int idx = gid * BV + v;
-                nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
+                nq[v] = qn > 0 ? ld_wg(&Q[idx < qn ? idx : qn - 1]) : -1;
             }
             for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
                 int u[BV], a0[BV], a1[BV];
@@ -313,6 +330,62 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
                 }
             }
+            // hubs: one wave per hub, its 64 / LB groups interleave the arcs
+            {
+                constexpr int GPW = 64 / LB;
+                const int wv = tid >> 6, NW = NT >> 6, gw = (tid & 63) / LB;
+                for (int h = wv; h < hn; h += NW) {
+                    const int u = ld_wg(&Q[NS - 1 - h]);
+                    const unsigned long long du0 = ld_wg(&D[(size_t)u * LB + l]);
+                    const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
+                    const bool act = b2d(du0) < bound;
+                    const bool defer = !act && du0 != INF_BITS;
+                    const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
+                    const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
+                    if (gw == 0 && l == 0 && dmask) atomicOr(&anyN[u >> 5], 1u << (u & 31));
+                    if (gw == 0 && defer) myMin = du0 < myMin ? du0 : myMin;
+                    const unsigned long long dub1 = act ? du0 : INF_BITS;
+                    if (!__ballot(amask != 0)) continue;       // wave-uniform
+                    if (gw == 0) {
+                        ++procs;
+                        arcsDone += a1 - a0;
+                        lanesAct += __popc(amask);
+                    }
+                    for (int t = a0 + gw * BK; t < a1; t += GPW * BK) {
+                        int xs[BK];
+                        double ws[BK];
+                        unsigned long long dx[BK];
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            const int a = t + k;
+                            const bool ok = a < a1;
+                            const Arc A = g.arcs[ok ? a : 0];
+                            xs[k] = ok ? A.col : -1;
+                            ws[k] = A.lat;
+                        }
+#pragma unroll
+                        for (int k = 0; k < BK; ++k)
+                            dx[k] = ld_wg(&D[(size_t)(xs[k] >= 0 ? xs[k] : 0) * LB + l]);
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            const int x = xs[k];
+                            bool imp = false;
+                            if (x >= 0) {
+                                const unsigned long long nb = d2b(b2d(dub1) + ws[k]);
+                                if (nb < dx[k]) {
+                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    imp = true;
+                                }
+                            }
+                            if (__ballot(imp) >> gbase & LBMASK && l == 0) {
+                                atomicOr(&anyN[x >> 5], 1u << (x & 31));
+                                myAct = 1;
+                            }
+                        }
+                    }
+                }
+            }
             if (dbg && l == 0) {
                 const unsigned long long bz = (unsigned long long)((long long)clock64() - tg0);
                 atomicMax(&ctl->busyMax, bz);
@@ -333,6 +406,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
             if (tid == 0) {
                 ctl->qtail = 0;
+                ctl->htail = 0;
                 ctl->active = 0;
                 ctl->minNext = INF_BITS;
                 if (dbg) {
