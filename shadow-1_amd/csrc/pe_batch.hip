@@ -239,6 +239,63 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             unsigned long long myMin = INF_BITS;
             int myAct = 0;
             const long long tg0 = dbg ? (long long)clock64() : 0;
+            // hubs first (their improvements reach the light vertices in this
+            // phase): one wave per hub, its 64 / LB groups interleave the arcs
+            {
+                constexpr int GPW = 64 / LB;
+                const int wv = tid >> 6, NW = NT >> 6, gw = (tid & 63) / LB;
+                for (int h = wv; h < hn; h += NW) {
+                    const int u = ld_wg(&Q[NS - 1 - h]);
+                    const unsigned long long du0 = ld_wg(&D[(size_t)u * LB + l]);
+                    const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
+                    const bool act = b2d(du0) < bound;
+                    const bool defer = !act && du0 != INF_BITS;
+                    const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
+                    const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
+                    if (gw == 0 && l == 0 && dmask) atomicOr(&anyN[u >> 5], 1u << (u & 31));
+                    if (gw == 0 && defer) myMin = du0 < myMin ? du0 : myMin;
+                    const unsigned long long dub1 = act ? du0 : INF_BITS;
+                    if (!__ballot(amask != 0)) continue;       // wave-uniform
+                    if (gw == 0) {
+                        ++procs;
+                        arcsDone += a1 - a0;
+                        lanesAct += __popc(amask);
+                    }
+                    for (int t = a0 + gw * BK; t < a1; t += GPW * BK) {
+                        int xs[BK];
+                        double ws[BK];
+                        unsigned long long dx[BK];
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            const int a = t + k;
+                            const bool ok = a < a1;
+                            const Arc A = g.arcs[ok ? a : 0];
+                            xs[k] = ok ? A.col : -1;
+                            ws[k] = A.lat;
+                        }
+#pragma unroll
+                        for (int k = 0; k < BK; ++k)
+                            dx[k] = ld_wg(&D[(size_t)(xs[k] >= 0 ? xs[k] : 0) * LB + l]);
+#pragma unroll
+                        for (int k = 0; k < BK; ++k) {
+                            const int x = xs[k];
+                            bool imp = false;
+                            if (x >= 0) {
+                                const unsigned long long nb = d2b(b2d(dub1) + ws[k]);
+                                if (nb < dx[k]) {
+                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    imp = true;
+                                }
+                            }
+                            if (__ballot(imp) >> gbase & LBMASK && l == 0) {
+                                atomicOr(&anyN[x >> 5], 1u << (x & 31));
+                                myAct = 1;
+                            }
+                        }
+                    }
+                }
+            }
             // the queue entries of the group's NEXT vertices are loaded one
             // iteration ahead (qn >= 1 here), so a vertex starts with its
             // dist / row-range loads instead of a dependent queue round trip
@@ -328,62 +385,6 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 myAct = 1;
                             }
                         }
-                }
-            }
-            // hubs: one wave per hub, its 64 / LB groups interleave the arcs
-            {
-                constexpr int GPW = 64 / LB;
-                const int wv = tid >> 6, NW = NT >> 6, gw = (tid & 63) / LB;
-                for (int h = wv; h < hn; h += NW) {
-                    const int u = ld_wg(&Q[NS - 1 - h]);
-                    const unsigned long long du0 = ld_wg(&D[(size_t)u * LB + l]);
-                    const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
-                    const bool act = b2d(du0) < bound;
-                    const bool defer = !act && du0 != INF_BITS;
-                    const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
-                    const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                    if (gw == 0 && l == 0 && dmask) atomicOr(&anyN[u >> 5], 1u << (u & 31));
-                    if (gw == 0 && defer) myMin = du0 < myMin ? du0 : myMin;
-                    const unsigned long long dub1 = act ? du0 : INF_BITS;
-                    if (!__ballot(amask != 0)) continue;       // wave-uniform
-                    if (gw == 0) {
-                        ++procs;
-                        arcsDone += a1 - a0;
-                        lanesAct += __popc(amask);
-                    }
-                    for (int t = a0 + gw * BK; t < a1; t += GPW * BK) {
-                        int xs[BK];
-                        double ws[BK];
-                        unsigned long long dx[BK];
-#pragma unroll
-                        for (int k = 0; k < BK; ++k) {
-                            const int a = t + k;
-                            const bool ok = a < a1;
-                            const Arc A = g.arcs[ok ? a : 0];
-                            xs[k] = ok ? A.col : -1;
-                            ws[k] = A.lat;
-                        }
-#pragma unroll
-                        for (int k = 0; k < BK; ++k)
-                            dx[k] = ld_wg(&D[(size_t)(xs[k] >= 0 ? xs[k] : 0) * LB + l]);
-#pragma unroll
-                        for (int k = 0; k < BK; ++k) {
-                            const int x = xs[k];
-                            bool imp = false;
-                            if (x >= 0) {
-                                const unsigned long long nb = d2b(b2d(dub1) + ws[k]);
-                                if (nb < dx[k]) {
-                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                                    imp = true;
-                                }
-                            }
-                            if (__ballot(imp) >> gbase & LBMASK && l == 0) {
-                                atomicOr(&anyN[x >> 5], 1u << (x & 31));
-                                myAct = 1;
-                            }
-                        }
-                    }
                 }
             }
             if (dbg && l == 0) {
