@@ -230,6 +230,8 @@ int shd_pe_synchronize(ShdPe* pe);
  * asks for it beside the spec peak; no reference counterpart. */
 int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbps);
 
+/* Counters of this engine (all its shards).  Both calls take the engine's
+ * compute lock: during a running compute they return once it is done. */
 int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out);
 int shd_pe_reset_stats(ShdPe* pe);
 

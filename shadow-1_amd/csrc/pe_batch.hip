@@ -18,10 +18,13 @@
 // the graph (host-side BFS rank), so their bucket frontiers coincide.
 //
 // Per batch:
-//   1. label-correcting delta-stepping with a shared bucket bound and
-//      double-buffered per-vertex pending lane masks (cur/next); relaxations
-//      are dist[u] + w only (left fold -> igraph's distances bit for bit,
-//      SURVEY.md Appendix B);
+//   1. label-correcting delta-stepping over per-lane keys (dist + the lane's
+//      shift: sources of one batch share a nearest hub, and the shift aligns
+//      their distances behind it) with one bucket bound, a near and a far
+//      pending bitmap (one bit per vertex), and per-ENTRY dirty bits: an entry
+//      is relaxed once per value it takes (dirty -> clean by CAS), not once per
+//      visit of its vertex; relaxations are dist[u] + w only (left fold ->
+//      igraph's distances bit for bit);
 //   2. predecessor pass: tight in-arc with minimum dist[u] per lane = igraph's
 //      first-popped tight predecessor; equal minima (or a zero-increment arc)
 //      mark the entry ambiguous (the row becomes a tie row for k_exact_rows
@@ -52,15 +55,40 @@ constexpr int WALK_BUDGET = 2048;   // walk steps per target before the deep-tre
 
 struct alignas(16) BCtrl {
     int qtail;
-    int active;
-    unsigned long long minNext;
+    int farAny;       // some vertex waits in the far set
+    unsigned long long farMin;   // smallest far key (bits of a non-negative double)
     unsigned int ambMask;
     int changed;
     int htail;        // heavy-vertex list (grows down from the top of the queue)
     int pad;
     unsigned long long busyMax;
     unsigned long long busySum;
+    double maxOff;    // largest lane offset of the batch (bits via atomicMax)
 };
+
+// Entry encoding of the [v][LB] distance array: (f64 bits << 1) | clean.
+// Positive doubles have bit 63 clear, so the shift loses nothing and the u64
+// order of encodings is the order of distances: an atomic min with a dirty
+// (clean = 0) encoding of a smaller distance always wins, an equal or larger
+// one never changes the distance.  A processor marks the value it relaxed
+// clean with a CAS, which fails (leaving the entry dirty) if an improvement
+// landed in between.
+__device__ __forceinline__ unsigned long long enc_dirty(unsigned long long bits) { return bits << 1; }
+__device__ __forceinline__ unsigned long long dec(unsigned long long e) { return e >> 1; }
+constexpr unsigned long long INF_ENC = (INF_BITS << 1) | 1ull;
+
+__device__ __forceinline__ void mark_clean(unsigned long long* p, unsigned long long e) {
+    unsigned long long expect = e;
+    (void)__hip_atomic_compare_exchange_strong(p, &expect, e | 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// bucket of a key: the smallest multiple of delta above it
+__device__ __forceinline__ double next_bound(double mn, double delta) {
+    double nb = (floor(mn / delta) + 1.0) * delta;
+    if (!(mn < nb)) nb = mn + delta;
+    return nb;
+}
 
 __device__ __forceinline__ void st_wg(int32_t* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -146,48 +174,55 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (b >= nBatches) break;
         const int row = batchRows[(size_t)b * LB + l];
         const int src = row >= 0 ? g.attached[row] : -1;
-        // ---- init: dist = +inf for all (v, lane); pending sets empty ----
+        // ---- init: dist = +inf (clean) for all (v, lane); pending sets empty ----
         {
             ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
             const size_t cnt2 = NE / 2;
-            const ulonglong2 inf2 = make_ulonglong2(INF_BITS, INF_BITS);
+            const ulonglong2 inf2 = make_ulonglong2(INF_ENC, INF_ENC);
             for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
             for (int w = tid; w < nwp; w += NT) { any0[w] = 0u; any1[w] = 0u; }
             if (tid == 0) {
                 ctl->qtail = 0;
-                ctl->active = 0;
-                ctl->minNext = INF_BITS;
+                ctl->farAny = 0;
+                ctl->farMin = INF_BITS;
                 ctl->ambMask = 0u;
                 ctl->changed = 0;
                 ctl->htail = 0;
-                        ctl->busyMax = 0;
+                ctl->busyMax = 0;
                 ctl->busySum = 0;
+                ctl->maxOff = 0.0;
             }
         }
         fence_wg();
         __syncthreads();
+        // lane offset: the source's distance to its nearest hub (host plan);
+        // key = dist + (maxOff - off) lines the lanes up behind the hub
+        const double off = (row >= 0 && bs.rowOff) ? as_global(bs.rowOff)[row] : 0.0;
+        if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
         if (gid == 0 && src >= 0) {
-            D[(size_t)src * LB + l] = d2b(0.0);
+            D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
             R[(size_t)src * LB + l] = 1.0;
             atomicOr(&any0[src >> 5], 1u << (src & 31));
         }
         fence_wg();
         __syncthreads();
+        const double sh = ctl->maxOff - off;      // >= 0: keys are non-negative
 
         // ================= 1. delta-stepping over the batch =================
-        // Pending state is one bit per VERTEX (LDS): "some lane of u improved".
-        // A candidate processes every lane with dist < bound: re-relaxing a
-        // lane that did not change costs no memory traffic (the group reads
-        // the whole dist[x][0..LB) line anyway) and never improves anything.
-        // Lanes at or above the bound keep the vertex pending (deferred);
-        // the bound only grows, so such a lane has never been processed at
-        // its current value.  Improvements are no-return atomic mins at
-        // workgroup scope: the line was just read for the pre-check, so the
-        // atomic resolves in L2, and no update is lost.  (Plain stores lost
-        // ~1 update per batch to concurrent groups, and the Bellman repair
-        // that caught it -- a second relax + predecessor pass -- cost 20% of
-        // the relax phase at C4.)  The Bellman check of pass 2 stays as the
-        // safety net.
+        // Pending state is one bit per VERTEX (LDS) in two sets: NEAR (some
+        // lane of u has a dirty value below the bound) and FAR (a dirty value
+        // at or above it).  A phase lists and clears the near set and
+        // processes each listed vertex: its dirty lanes below the bound are
+        // marked clean (CAS on the value read) and relaxed, its dirty lanes
+        // at or above the bound send it to the far set.  Clean lanes are
+        // never re-relaxed (their value already reached every out-neighbour),
+        // so a vertex costs arc traffic only when a lane has a new value.
+        // When the near set is empty the bound moves to the bucket of the
+        // smallest far key and the far set becomes the near set.
+        // Improvements are no-return atomic mins at workgroup scope on the
+        // encoding (the line was just read for the pre-check, so the atomic
+        // resolves in L2, and no update is lost).  The Bellman check of pass
+        // 2 stays as the safety net.
         const long long tPh0 = dbg ? (long long)clock64() : 0;
         long long tPh1 = 0;
         int par = 0, phases = 0, repairs = 0;
@@ -195,11 +230,12 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         const int phaseCap = 8 * n + 1024;
         long long procs = 0, arcsDone = 0, lanesAct = 0;
         double bound = delta;
+        unsigned long long myFar = INF_BITS;      // smallest far key this thread added
         for (;;) {   // phases + verification until the Bellman check holds
         for (;;) {
-            uint32_t* const anyC = par ? any1 : any0;
-            uint32_t* const anyN = par ? any0 : any1;
-            // candidates = vertices with a pending bit (cur set, consumed)
+            uint32_t* const anyC = par ? any1 : any0;   // near
+            uint32_t* const anyF = par ? any0 : any1;   // far
+            // candidates = vertices with a near bit (consumed)
             // (hubs -- degree >= the engine's heavy threshold -- go to a list
             // of their own, processed by whole waves: one 16-lane group on a
             // hub's ~1000 arcs would set the phase's length)
@@ -227,17 +263,35 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     }
                 }
             }
+            if (myFar != INF_BITS) {
+                atomicMin(&ctl->farMin, myFar);
+                myFar = INF_BITS;
+            }
             fence_wg();
             __syncthreads();
             const int qn = ctl->qtail;
             const int hn = ctl->htail;
-            if (qn == 0 && hn == 0) break;
+            if (qn == 0 && hn == 0) {
+                // bucket settled: advance to the far set, or done
+                const int farAny = ctl->farAny;
+                const double fm = b2d(ctl->farMin);
+                __syncthreads();
+                if (!farAny) break;
+                bound = fm < b2d(INF_BITS) ? next_bound(fm, delta) : b2d(INF_BITS);
+                if (tid == 0) {
+                    ctl->farAny = 0;
+                    ctl->farMin = INF_BITS;
+                }
+                par ^= 1;
+                ++phases;
+                __syncthreads();
+                continue;
+            }
             if (phases > phaseCap) {        // safety net: never spin the GPU
                 failed = true;
                 break;
             }
-            unsigned long long myMin = INF_BITS;
-            int myAct = 0;
+            int farAdd = 0;
             const long long tg0 = dbg ? (long long)clock64() : 0;
             // hubs first (their improvements reach the light vertices in this
             // phase): one wave per hub, its 64 / LB groups interleave the arcs
@@ -246,15 +300,22 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 const int wv = tid >> 6, NW = NT >> 6, gw = (tid & 63) / LB;
                 for (int h = wv; h < hn; h += NW) {
                     const int u = ld_wg(&Q[NS - 1 - h]);
-                    const unsigned long long du0 = ld_wg(&D[(size_t)u * LB + l]);
+                    unsigned long long* const pu = &D[(size_t)u * LB + l];
+                    const unsigned long long e0 = ld_wg(pu);
                     const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
-                    const bool act = b2d(du0) < bound;
-                    const bool defer = !act && du0 != INF_BITS;
+                    const double k0 = b2d(dec(e0)) + sh;
+                    const bool dirty = !(e0 & 1ull);
+                    const bool act = dirty && k0 < bound;
+                    const bool defer = dirty && !(k0 < bound);
                     const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
                     const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                    if (gw == 0 && l == 0 && dmask) atomicOr(&anyN[u >> 5], 1u << (u & 31));
-                    if (gw == 0 && defer) myMin = du0 < myMin ? du0 : myMin;
-                    const unsigned long long dub1 = act ? du0 : INF_BITS;
+                    if (gw == 0 && l == 0 && dmask) atomicOr(&anyF[u >> 5], 1u << (u & 31));
+                    if (gw == 0 && defer) {
+                        myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
+                        farAdd = 1;
+                    }
+                    if (gw == 0 && act) mark_clean(pu, e0);
+                    const unsigned long long dub1 = act ? dec(e0) : INF_BITS;
                     if (!__ballot(amask != 0)) continue;       // wave-uniform
                     if (gw == 0) {
                         ++procs;
@@ -279,18 +340,26 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const int x = xs[k];
-                            bool imp = false;
+                            bool impN = false, impF = false;
                             if (x >= 0) {
-                                const unsigned long long nb = d2b(b2d(dub1) + ws[k]);
-                                if (nb < dx[k]) {
-                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                const double nd = b2d(dub1) + ws[k];
+                                const unsigned long long nb = d2b(nd);
+                                if (nb < dec(dx[k])) {
+                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], enc_dirty(nb), __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-                                    imp = true;
+                                    const double kx = nd + sh;
+                                    impN = kx < bound;
+                                    impF = !impN;
+                                    if (impF) myFar = d2b(kx) < myFar ? d2b(kx) : myFar;
                                 }
                             }
-                            if (__ballot(imp) >> gbase & LBMASK && l == 0) {
-                                atomicOr(&anyN[x >> 5], 1u << (x & 31));
-                                myAct = 1;
+                            const uint64_t bn = __ballot(impN), bf = __ballot(impF);
+                            if (l == 0) {
+                                if ((bn >> gbase) & LBMASK) atomicOr(&anyC[x >> 5], 1u << (x & 31));
+                                if ((bf >> gbase) & LBMASK) {
+                                    atomicOr(&anyF[x >> 5], 1u << (x & 31));
+                                    farAdd = 1;
+                                }
                             }
                         }
                     }
@@ -321,20 +390,26 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const int uc = u[v] >= 0 ? u[v] : 0;
                     const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
                     const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
-                    db[v] = u[v] >= 0 ? d0 : INF_BITS;
+                    db[v] = u[v] >= 0 ? d0 : INF_ENC;
                     a0[v] = u[v] >= 0 ? r0 : 0;
                     a1[v] = u[v] >= 0 ? r1 : 0;
                 }
                 int maxd = 0;
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    const bool act = b2d(db[v]) < bound;
-                    const bool defer = !act && db[v] != INF_BITS;
+                    const double k0 = b2d(dec(db[v])) + sh;
+                    const bool dirty = !(db[v] & 1ull);
+                    const bool act = dirty && k0 < bound;
+                    const bool defer = dirty && !(k0 < bound);
                     const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
                     const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                    if (l == 0 && dmask) atomicOr(&anyN[u[v] >> 5], 1u << (u[v] & 31));
-                    if (defer) myMin = db[v] < myMin ? db[v] : myMin;
-                    dub[v] = act ? db[v] : INF_BITS;
+                    if (l == 0 && dmask) atomicOr(&anyF[u[v] >> 5], 1u << (u[v] & 31));
+                    if (defer) {
+                        myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
+                        farAdd = 1;
+                    }
+                    if (act) mark_clean(&D[(size_t)u[v] * LB + l], db[v]);
+                    dub[v] = act ? dec(db[v]) : INF_BITS;
                     if (!amask) a1[v] = a0[v];
                     else {
                         ++procs;
@@ -343,7 +418,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     }
                     maxd = max(maxd, a1[v] - a0[v]);
                 }
-                // relax u's out-arcs for the lanes below the bound
+                // relax u's out-arcs for the dirty lanes below the bound
                 for (int t = 0; t < maxd; t += BK) {
                     int xs[BV][BK];
                     double ws[BV][BK];
@@ -371,18 +446,26 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const int x = xs[v][k];
-                            bool imp = false;
+                            bool impN = false, impF = false;
                             if (x >= 0) {
-                                const unsigned long long nb = d2b(b2d(dub[v]) + ws[v][k]);
-                                if (nb < dx[v][k]) {
-                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], nb, __ATOMIC_RELAXED,
+                                const double nd = b2d(dub[v]) + ws[v][k];
+                                const unsigned long long nb = d2b(nd);
+                                if (nb < dec(dx[v][k])) {
+                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], enc_dirty(nb), __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-                                    imp = true;
+                                    const double kx = nd + sh;
+                                    impN = kx < bound;
+                                    impF = !impN;
+                                    if (impF) myFar = d2b(kx) < myFar ? d2b(kx) : myFar;
                                 }
                             }
-                            if (__ballot(imp) >> gbase & LBMASK && l == 0) {
-                                atomicOr(&anyN[x >> 5], 1u << (x & 31));
-                                myAct = 1;
+                            const uint64_t bn = __ballot(impN), bf = __ballot(impF);
+                            if (l == 0) {
+                                if ((bn >> gbase) & LBMASK) atomicOr(&anyC[x >> 5], 1u << (x & 31));
+                                if ((bf >> gbase) & LBMASK) {
+                                    atomicOr(&anyF[x >> 5], 1u << (x & 31));
+                                    farAdd = 1;
+                                }
                             }
                         }
                 }
@@ -392,24 +475,12 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 atomicMax(&ctl->busyMax, bz);
                 atomicAdd(&ctl->busySum, bz);
             }
-            if (myMin != INF_BITS) atomicMin(&ctl->minNext, myMin);
-            if (myAct) ctl->active = 1;
+            if (farAdd) ctl->farAny = 1;
             fence_wg();
-            __syncthreads();
-            if (!ctl->active) {
-                // no relaxation improved anything: the bucket is settled, jump
-                // to the bucket of the smallest deferred distance
-                const double mn = b2d(ctl->minNext);
-                double nb = (floor(mn / delta) + 1.0) * delta;
-                if (!(mn < nb)) nb = mn + delta;
-                bound = nb;
-            }
             __syncthreads();
             if (tid == 0) {
                 ctl->qtail = 0;
                 ctl->htail = 0;
-                ctl->active = 0;
-                ctl->minNext = INF_BITS;
                 if (dbg) {
                     dbg[16 * b + 12] += (int)(ctl->busyMax >> 10);
                     dbg[16 * b + 13] += (int)((ctl->busySum / NG) >> 10);
@@ -418,7 +489,6 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     ctl->busySum = 0;
                 }
             }
-            par ^= 1;
             ++phases;
             __syncthreads();
         }
@@ -443,7 +513,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 for (int v = 0; v < BV; ++v) {
                     const int vv = v0 + v;
                     if (vv < n) {
-                        dvb[v] = ld_wg(&D[(size_t)vv * LB + l]);
+                        dvb[v] = dec(ld_wg(&D[(size_t)vv * LB + l]));
                         a0[v] = undirected ? g.rowPtr[vv] : g.inPtr[vv];
                         a1[v] = undirected ? g.rowPtr[vv + 1] : g.inPtr[vv + 1];
                     } else {
@@ -487,7 +557,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const unsigned long long t2 =
-                                ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]);
+                                dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]));
                             du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
                         }
 #pragma unroll
@@ -517,7 +587,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const size_t e = (size_t)vv * LB + l;
                     const bool bad = !root[v] && mn[v] < dvb[v];
                     if (bad) {
-                        D[e] = mn[v];
+                        D[e] = enc_dirty(mn[v]);
                         viol = 1;
                     }
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
@@ -603,7 +673,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     }
                 } else {
                     const size_t e = (size_t)t * LB + l;
-                    const unsigned long long dt = ld_wg(&D[e]);
+                    const unsigned long long dt = dec(ld_wg(&D[e]));
                     if (dt == INF_BITS) {
                         f |= F_UNREACHABLE;
                     } else {
@@ -757,17 +827,17 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 const int pe = ld_wg(&P[e]);
                 const bool am = pe >= 0 && (pe & TIE_AMB);
                 const size_t o = (size_t)sl * (size_t)tie.n + v;
-                tie.D[o] = b2d(ld_wg(&D[e]));
+                tie.D[o] = b2d(dec(ld_wg(&D[e])));
                 tie.P[o] = pe;
                 if (am) {   // rare: re-derive the tied (minimum tight) predecessor distance
-                    const unsigned long long dv = ld_wg(&D[e]);
+                    const unsigned long long dv = dec(ld_wg(&D[e]));
                     const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];
                     const int a1 = undirected ? g.rowPtr[v + 1] : g.inPtr[v + 1];
                     unsigned long long mt = INF_BITS;
                     for (int a = a0; a < a1; ++a) {
                         const int u = undirected ? g.col[a] : g.inCol[a];
                         const double w = undirected ? g.lat[a] : g.inLat[a];
-                        const unsigned long long du = ld_wg(&D[(size_t)u * LB + l]);
+                        const unsigned long long du = dec(ld_wg(&D[(size_t)u * LB + l]));
                         if (du <= dv && d2b(b2d(du) + w) == dv && du < mt) mt = du;
                     }
                     if (mt != INF_BITS) thr = mt > thr ? mt : thr;

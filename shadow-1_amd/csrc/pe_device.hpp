@@ -74,8 +74,8 @@ struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0;
-    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 0, batchWpe = 0;
-    double batchDeltaFactor = 8.0, batchScratchGB = 64.0;
+    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 1, batchWpe = 0;
+    double batchDeltaFactor = 1.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
     int debug = 0, streamWgPerCU = 4;
@@ -106,6 +106,8 @@ struct BatchScratch {
     int32_t* queue;          // [slot][nStride] phase candidate list
     int32_t* next;           // next batch to take (device counter, zeroed per launch)
     int64_t nStride;         // >= n, multiple of 64
+    const double* rowOff;    // [T] per table position: the source's distance to its
+                             // batch hub (bucket key offset; null = no offsets)
 };
 
 struct BatchLaunch {

@@ -92,7 +92,8 @@ struct ShdPe {
     Tuning tu{};
     int mode = 1;
     bool batched = false;
-    std::vector<int32_t> rank;       // table position -> BFS visit rank
+    std::vector<int32_t> rank;       // table position -> batch order rank
+    std::vector<double> rowOff;      // table position -> distance to its batch hub (order 1)
     int G = 1;                       // global row shards
     std::vector<int32_t> bounds;     // G + 1 position bounds
     int firstShard = 0;              // global index of shards[0]
@@ -305,11 +306,15 @@ static int configure(ShdPe* pe, Shard* sh) {
 // Batch order of the table positions: sources of one batch should have
 // similar distance profiles so their delta-stepping frontiers coincide.
 //   order 0: BFS visit rank (components in vertex order);
-//   order 1: nearest-hub cells -- a multi-source Dijkstra from the K
-//            highest-degree vertices gives every vertex its closest hub;
-//            sources sort by (hub, distance to it), so a batch holds
-//            sources that reach the rest of the graph through one hub.
-// Scheduling only: results never depend on it.
+//   order 1 (default): nearest-hub cells -- a multi-source Dijkstra from
+//            the K highest-degree vertices gives every vertex its closest
+//            hub; sources sort by (hub, distance to it), so a batch holds
+//            sources that reach the rest of the graph through one hub, and
+//            the distance to the hub becomes the lane's bucket key offset
+//            (k_batch_rows: a lane's key is dist + maxOff - off).
+// Scheduling only: results never depend on it (tools/sim/ models the
+// schedule: C4 arc visits 3.9 -> 2.2 x m per batch with offsets, dirty
+// lanes and a far set at delta = mean arc latency).
 static void compute_ranks(ShdPe* pe) {
     const HostGraph& g = pe->hg;
     std::vector<int32_t> order;
@@ -345,6 +350,13 @@ static void compute_ranks(ShdPe* pe) {
         std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
             return owner[a] != owner[b] ? owner[a] < owner[b] : dist[a] < dist[b];
         });
+        // bucket key offsets: a source's distance to its hub, so the lanes of
+        // a batch reach the vertices behind the hub in the same bucket
+        pe->rowOff.assign(pe->attached.size(), 0.0);
+        for (size_t p = 0; p < pe->attached.size(); ++p) {
+            const double d = dist[pe->attached[p]];
+            pe->rowOff[p] = std::isfinite(d) ? d : 0.0;
+        }
     } else {
         std::vector<uint8_t> seen(g.n, 0);
         for (int32_t r = 0; r < g.n; ++r) {
@@ -685,6 +697,12 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.queue = (int32_t*)q;
     sh->bsc.next = (int32_t*)q + slots * NS;
     sh->bsc.nStride = (int64_t)NS;
+    sh->bsc.rowOff = nullptr;
+    if (!pe->rowOff.empty()) {
+        double* ro;
+        if ((rc = dev_upload(sh, &ro, pe->rowOff))) return rc;
+        sh->bsc.rowOff = ro;
+    }
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
     if ((rc = ensure_tie(pe, sh))) return rc;
@@ -858,6 +876,28 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                              [&](int32_t a, int32_t b) { return pe->rank[a] < pe->rank[b]; });
             const int32_t nB = (cnt + LB - 1) / LB;
             order.resize((size_t)nB * LB, -1);
+            if (!pe->rowOff.empty() && nB > 1) {
+                // longest batches first (workgroups take batches in order, so
+                // the last round is made of short ones): a batch's cost grows
+                // with its sources' mean distance to their hub (tools/sim/:
+                // correlation 0.53 with arc visits at C4)
+                std::vector<std::pair<double, int32_t>> key(nB);
+                for (int32_t b = 0; b < nB; ++b) {
+                    double s = 0.0;
+                    int c = 0;
+                    for (int l = 0; l < LB; ++l) {
+                        const int32_t p = order[(size_t)b * LB + l];
+                        if (p >= 0) { s += pe->rowOff[p]; ++c; }
+                    }
+                    key[b] = {c ? -s / c : 0.0, b};
+                }
+                std::stable_sort(key.begin(), key.end());
+                std::vector<int32_t> re((size_t)nB * LB);
+                for (int32_t i = 0; i < nB; ++i)
+                    std::copy(order.begin() + (size_t)key[i].second * LB,
+                              order.begin() + (size_t)(key[i].second + 1) * LB, re.begin() + (size_t)i * LB);
+                order.swap(re);
+            }
             HIPCHK(hipMemcpyAsync(sh->dBatchRows, order.data(), order.size() * 4,
                                   hipMemcpyHostToDevice, sh->stream));
             if (sh->dDbg) HIPCHK(hipMemsetAsync(sh->dDbg, 0, (size_t)nB * 64, sh->stream));
@@ -1187,6 +1227,9 @@ extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, 
     if (count == 0) return SHD_PE_OK;
     int rc = ensure_rows(pe, start, count);       // same contract as shd_pe_get_rows
     if (rc) return rc;
+    // table_pieces reads gathered / the full table, which shd_pe_gather
+    // writes under copyMu
+    std::lock_guard<std::mutex> lk(pe->copyMu);
     std::vector<Piece> pieces;
     if ((rc = table_pieces(pe, start, count, pieces))) return rc;
     const size_t T = pe->attached.size();
@@ -1255,11 +1298,29 @@ static int gather_locked(ShdPe* pe) {
     std::vector<Field> fields;
     table_fields(pe, fields);
     const size_t ts = (size_t)T;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
     Shard* s0 = pe->shards[0].get();
+    bool distinct = true;
+    for (size_t i = 0; i < pe->shards.size(); ++i)
+        for (size_t j = 0; j < i; ++j)
+            if (pe->shards[i]->device == pe->shards[j]->device) distinct = false;
+    // in-process RCCL over xGMI (distinct devices): one communicator per
+    // device, created before the timed region
+    if (pe->G > 1 && !pe->xcomm && distinct && !s0->comm) {
+        std::vector<ncclComm_t> comms(pe->shards.size());
+        std::vector<int> devs;
+        for (auto& s : pe->shards) devs.push_back(s->device);
+        if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess)
+            return SHD_PE_ECOMM;
+        for (size_t i = 0; i < comms.size(); ++i) pe->shards[i]->comm = comms[i];
+    }
+    struct Events {   // destroyed on every exit path
+        hipEvent_t e[2] = {nullptr, nullptr};
+        ~Events() { for (hipEvent_t x : e) if (x) (void)hipEventDestroy(x); }
+    } ev;
     HIPCHK(hipSetDevice(s0->device));
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventCreate(&ev.e[0]));
+    HIPCHK(hipEventCreate(&ev.e[1]));
+    hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
     HIPCHK(hipEventRecord(e0, s0->stream));
     if (pe->G == 1) {
         // nothing to exchange
@@ -1282,20 +1343,8 @@ static int gather_locked(ShdPe* pe) {
         if (ncclGroupEnd() != ncclSuccess) rc = SHD_PE_ECOMM;
         if (rc) return rc;
     } else {
-        bool distinct = true;
-        for (size_t i = 0; i < pe->shards.size(); ++i)
-            for (size_t j = 0; j < i; ++j)
-                if (pe->shards[i]->device == pe->shards[j]->device) distinct = false;
         if (distinct) {
-            // in-process RCCL over xGMI: one communicator per device
-            if (!s0->comm) {
-                std::vector<ncclComm_t> comms(pe->shards.size());
-                std::vector<int> devs;
-                for (auto& s : pe->shards) devs.push_back(s->device);
-                if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess)
-                    return SHD_PE_ECOMM;
-                for (size_t i = 0; i < comms.size(); ++i) pe->shards[i]->comm = comms[i];
-            }
+            // in-process RCCL over xGMI: a group of per-shard broadcasts
             if (ncclGroupStart() != ncclSuccess) return SHD_PE_ECOMM;
             for (size_t r = 0; r < pe->shards.size(); ++r) {
                 Shard* root = pe->shards[r].get();
@@ -1339,8 +1388,6 @@ static int gather_locked(ShdPe* pe) {
     HIPCHK(hipEventRecord(e1, s0->stream));
     HIPCHK(hipEventSynchronize(e1));
     pe->msGather += elapsed(e0, e1);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     for (int32_t p = 0; p < T; ++p) pe->rowDone[p].store(1, std::memory_order_release);
     pe->gathered = true;
     return SHD_PE_OK;
@@ -1477,6 +1524,9 @@ extern "C" int shd_pe_attached(const ShdPe* pe, int32_t* out) {
 
 extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
     if (!pe || !out) return SHD_PE_EINVAL;
+    // compute updates the per-shard stats under mu: snapshot under it too
+    // (a call during a compute returns once that compute is done)
+    std::lock_guard<std::mutex> lk(const_cast<ShdPe*>(pe)->mu);
     ShdPeStats t = pe->shards[0]->stats;
     for (size_t i = 1; i < pe->shards.size(); ++i) {
         const ShdPeStats& s = pe->shards[i]->stats;
@@ -1504,6 +1554,7 @@ extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
 
 extern "C" int shd_pe_reset_stats(ShdPe* pe) {
     if (!pe) return SHD_PE_EINVAL;
+    std::lock_guard<std::mutex> lk(pe->mu);
     for (auto& sp : pe->shards) {
         ShdPeStats& st = sp->stats;
         ShdPeStats keep = st;

@@ -391,6 +391,10 @@ class RowStore:
         rel = np.ascontiguousarray(rel, dtype=np.float64)
         flags = np.ascontiguousarray(flags, dtype=np.uint8)
         adj = None if adjacent is None else np.ascontiguousarray(adjacent, dtype=np.uint8)
+        T = self._att.shape[0]           # the C side reads T entries of each array
+        for name, arr in (("lat", lat), ("rel", rel), ("flags", flags), ("adjacent", adj)):
+            if arr is not None and arr.shape[0] < T:
+                raise ValueError(f"store_row: {name} has {arr.shape[0]} entries, need {T}")
         rc = self._lib.shd_rowstore_store_row(self.h, int(s), _p(lat), _p(rel), _p(flags),
                                               int(is_complete), _p(adj))
         if rc < 0:

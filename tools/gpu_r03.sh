@@ -1,0 +1,42 @@
+#!/bin/bash
+# Round-3 GPU pass.  Stages (space-separated in $STAGES):
+#   tests   pytest -m gpu (PYTEST_K filters)
+#   bench   bench.py lines for $WLS (no CPU leg, no tie stress)
+#   ab      same-box A/B: libshdpe_head.so vs libshdpe.so on $WLS, twice each
+#   debug   SHDPE_DEBUG counters of k_batch_rows on $DEBUG_WL
+#   relabel tools/relabel_probe.py
+# usage: STAGES="tests bench" tools/gpu_r03.sh TAG
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R
+TAG=${1:-r03}; OUT=gpurun_out/$TAG; mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+WLS=${WLS:-c4}
+line() { python3 -c "import json,sys; d=json.load(open('$1')); r=d['roofline']; print('$2', round(d['value']), 'rows/s', round(d['ms_per_step'],2), 'ms/step', 'kernel', round(r['avg_launch_ms'],2), 'ms frac', round(r['frac'],4), 'exact', round(d['ms_exact_per_step'],2))"; }
+for st in ${STAGES:-tests bench}; do
+  case $st in
+  tests)
+    timeout -k 10 1100 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/tests.log 2>&1
+    rc=$?; tail -3 $OUT/tests.log; [ $rc = 0 ] || { grep -E "FAIL|Error|error|assert" $OUT/tests.log | head -30; exit $rc; } ;;
+  bench)
+    for wl in ${WLS//,/ }; do
+      timeout -k 10 300 python3 -u bench.py --workload $wl --steps ${STEPS:-3} --warmup 1 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $OUT/bench_$wl.json 2> $OUT/bench_$wl.err || { tail -20 $OUT/bench_$wl.err; exit 1; }
+      line $OUT/bench_$wl.json $wl
+    done ;;
+  ab)
+    for wl in ${WLS//,/ }; do
+      for rep in 1 2; do
+        for lib in head new; do
+          L=shadow-1_amd/libshdpe.so; [ $lib = head ] && L=shadow-1_amd/libshdpe_head.so
+          SHDPE_LIB=$R/$L timeout -k 10 300 python3 -u bench.py --workload $wl --steps 3 --warmup 1 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $OUT/ab_${wl}_$lib.json 2> $OUT/ab_${wl}_$lib.err || { tail -20 $OUT/ab_${wl}_$lib.err; exit 1; }
+          line $OUT/ab_${wl}_$lib.json "$wl $lib #$rep"
+        done
+      done
+    done ;;
+  debug)
+    SHDPE_DEBUG=1 timeout -k 10 300 python3 -u bench.py --workload ${DEBUG_WL:-c4} --steps 1 --warmup 0 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $OUT/debug.json 2> $OUT/debug.err || { tail -20 $OUT/debug.err; exit 1; }
+    grep shdpe $OUT/debug.err | head -20 ;;
+  relabel)
+    timeout -k 10 400 python3 -u tools/relabel_probe.py ${RELABEL_WL:-c4} > $OUT/relabel.txt 2>&1 || { tail -20 $OUT/relabel.txt; exit 1; }
+    cat $OUT/relabel.txt ;;
+  esac
+done

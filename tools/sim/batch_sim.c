@@ -1,0 +1,143 @@
+// Host simulation of k_batch_rows' relaxation schedule (scheduling probe,
+// not product code): counts vertex processings / arc visits per batch for a
+// given bucket width and per-lane bucket offsets, so batch orders and bucket
+// rules can be compared on the CPU before a GPU run.
+//
+// Phase model: candidates = vertices pending at the phase start, processed
+// in place (Gauss-Seidel) hubs first then ascending id, like the kernel's
+// queue; a vertex's lanes with key = dist - off < bound relax all arcs, the
+// other reached lanes keep it pending; the bound advances to the bucket of
+// the smallest deferred key only after a phase with no improvement.
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+    double procs, arcs, phases, lanesAct, cands;
+} SimOut;
+
+int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double* lat,
+              const int32_t* srcs, const double* offs, int32_t nBatch, int32_t LB, double delta,
+              int32_t heavyDeg, int32_t dirtyMode, int32_t farMode, SimOut* out) {
+    double* D = malloc(sizeof(double) * (size_t)n * LB);
+    uint8_t* pend = calloc(n, 1);
+    uint8_t* nextp = calloc(n, 1);
+    int32_t* q = malloc(sizeof(int32_t) * n);
+    uint64_t* dirty = calloc(n, 8);
+    uint8_t* farp = calloc(n, 1);
+    if (!D || !pend || !nextp || !q) return -1;
+    memset(out, 0, sizeof(*out));
+    for (int b = 0; b < nBatch; ++b) {
+        const int32_t* s = srcs + (size_t)b * LB;
+        const double* off = offs + (size_t)b * LB;
+        for (size_t i = 0; i < (size_t)n * LB; ++i) D[i] = INFINITY;
+        memset(pend, 0, n);
+        memset(dirty, 0, 8 * (size_t)n);
+        memset(farp, 0, n);
+        double farMin = INFINITY;
+        double maxOff = 0;
+        for (int l = 0; l < LB; ++l) {
+            if (s[l] < 0) continue;
+            D[(size_t)s[l] * LB + l] = 0.0;
+            dirty[s[l]] |= 1ull << l;
+            pend[s[l]] = 1;
+            if (off[l] > maxOff) maxOff = off[l];
+        }
+        double bound = -maxOff + delta;
+        // start at the bucket of the smallest source key
+        {
+            double mk = INFINITY;
+            for (int l = 0; l < LB; ++l)
+                if (s[l] >= 0 && -off[l] < mk) mk = -off[l];
+            bound = (floor(mk / delta) + 1.0) * delta;
+        }
+        for (int guard = 0; guard < 100000; ++guard) {
+            int qn = 0;
+            for (int v = 0; v < n; ++v)
+                if (pend[v] && rowPtr[v + 1] - rowPtr[v] >= heavyDeg) q[qn++] = v;
+            for (int v = 0; v < n; ++v)
+                if (pend[v] && rowPtr[v + 1] - rowPtr[v] < heavyDeg) q[qn++] = v;
+            if (qn == 0) {
+                if (!farMode || farMin == INFINITY) break;
+                const double mn = farMin;
+                farMin = INFINITY;
+                double nb = (floor(mn / delta) + 1.0) * delta;
+                if (!(mn < nb)) nb = mn + delta;
+                bound = nb;
+                memcpy(pend, farp, n);
+                memset(farp, 0, n);
+                continue;
+            }
+            memset(pend, 0, n);
+            memset(nextp, 0, n);
+            int active = 0;
+            double minNext = INFINITY;
+            out->cands += qn;
+            for (int i = 0; i < qn; ++i) {
+                const int u = q[i];
+                double du[64];
+                uint64_t act = 0;
+                for (int l = 0; l < LB; ++l) {
+                    du[l] = D[(size_t)u * LB + l];
+                    if (du[l] == INFINITY) continue;
+                    const double key = du[l] - off[l];
+                    if (key < bound) act |= 1ull << l;
+                    else if (farMode) {
+                        farp[u] = 1;
+                        if (key < farMin) farMin = key;
+                    } else {
+                        nextp[u] = 1;
+                        if (key < minNext) minNext = key;
+                    }
+                }
+                if (dirtyMode) {
+                    uint64_t dm = 0;
+                    const uint64_t gmask = dirtyMode >= 64 ? ~0ull : ((1ull << dirtyMode) - 1);
+                    for (int g0 = 0; g0 < LB; g0 += dirtyMode)
+                        if ((dirty[u] >> g0) & gmask) dm |= gmask << g0;
+                    act &= dm;
+                }
+                if (!act) continue;
+                dirty[u] &= ~act;
+                out->procs += 1;
+                out->lanesAct += __builtin_popcountll(act);
+                out->arcs += rowPtr[u + 1] - rowPtr[u];
+                for (int a = rowPtr[u]; a < rowPtr[u + 1]; ++a) {
+                    const int x = col[a];
+                    const double w = lat[a];
+                    for (int l = 0; l < LB; ++l) {
+                        if (!((act >> l) & 1)) continue;
+                        const double nb = du[l] + w;
+                        if (nb < D[(size_t)x * LB + l]) {
+                            D[(size_t)x * LB + l] = nb;
+                            if (farMode && nb - off[l] >= bound) {
+                                farp[x] = 1;
+                                if (nb - off[l] < farMin) farMin = nb - off[l];
+                            } else {
+                                nextp[x] = 1;
+                            }
+                            dirty[x] |= 1ull << l;
+                            active = 1;
+                        }
+                    }
+                }
+            }
+            memcpy(pend, nextp, n);
+            out->phases += 1;
+            if (!active && !farMode) {
+                const double mn = minNext;
+                double nb = (floor(mn / delta) + 1.0) * delta;
+                if (!(mn < nb)) nb = mn + delta;
+                bound = nb;
+            }
+        }
+    }
+    free(D);
+    free(pend);
+    free(nextp);
+    free(q);
+    free(dirty);
+    free(farp);
+    return 0;
+}
