@@ -113,13 +113,18 @@ def tie_positions(eng, E):
 
 def whole_table_properties(eng, ctx):
     """Every row: no failures (connected, self-loops), latency > 0,
-    reliability in (0, 1], hops >= 1, pred a vertex id."""
+    reliability in (0, 1], hops >= 1, pred a vertex id off the diagonal
+    (the 1-vertex path [s] has no predecessor: pred -1, as the oracle)."""
     for start in range(0, eng.T, 1024):
-        blk = eng.get_rows(start, min(1024, eng.T - start))
+        cnt = min(1024, eng.T - start)
+        blk = eng.get_rows(start, cnt)
         assert not np.any(blk["flags"] & 0x03), f"{ctx} failed entries in rows {start}.."
         assert np.all(blk["lat"] > 0) and np.all((blk["rel"] > 0) & (blk["rel"] <= 1)), ctx
         assert np.all(blk["hops"] >= 1), ctx
-        assert np.all(blk["pred"] >= 0), ctx
+        diag = np.zeros(blk["pred"].shape, bool)
+        diag[np.arange(cnt), start + np.arange(cnt)] = True
+        assert np.all(blk["pred"][~diag] >= 0), ctx
+        assert np.all(blk["pred"][diag] == -1), ctx
 
 
 # ---------------------------------------------------------------------------
