@@ -84,10 +84,16 @@ def cpu_baseline(top, att, budget_s=12.0, max_rows=4000, threads=1):
 
 
 def load_traffic(workload):
+    """PMC traffic of the dominant kernel (profiles/traffic_<wl>.json, made by
+    tools/traffic_json.py) -- only if it was measured on a library built from
+    the same kernel sources as this one; a stale capture is dropped."""
+    from shdpe.engine import kernel_source_hash
     p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
     if os.path.exists(p):
         with open(p) as f:
-            return json.load(f)
+            t = json.load(f)
+        if t.get("src_hash") == kernel_source_hash():
+            return t
     return None
 
 
@@ -239,6 +245,7 @@ def main():
         "roofline": {"bound": bound, "kernel": kname, "achieved": achieved,
                      "peak": peak, "unit": unit, "frac": achieved / peak,
                      "traffic": traffic_bytes,
+                     "traffic_tag": (traffic or {}).get("tag"),
                      "algorithmic_per_launch": bytes_per_launch,
                      "avg_launch_ms": avg_launch_ms, "launches": launches},
         "rows_exact": st["rowsExact"] // max(1, args.steps),

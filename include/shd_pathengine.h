@@ -226,7 +226,8 @@ int shd_pe_synchronize(ShdPe* pe);
 
 /* Measurement helper (not on the path): achievable HBM bandwidth of this
  * engine's device, a 16-B streaming copy of `bytes` (read + write counted),
- * averaged over `iters` launches on the engine's stream.  SURVEY.md §8(d)
+ * averaged over `iters` launches on the engine's stream; the best of several
+ * copy shapes (cache policy, loads in flight, workgroups per CU).  SURVEY.md §8(d)
  * asks for it beside the spec peak; no reference counterpart. */
 int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbps);
 

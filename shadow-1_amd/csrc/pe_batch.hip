@@ -732,6 +732,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         h = he;
                         const int pa = ld_wg(&P[e]);
                         pv = pa >= 0 ? g.inCol[pa & ~TIE_AMB] : -1;
+                        if (pv >= 0 && g.oldId) pv = g.oldId[pv];   // device id -> caller's id
                         if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
                             Rl = re;
                         else

@@ -53,6 +53,9 @@ struct DevGraph {
     const int32_t* attached;   // [T]
     const uint8_t* isAttached; // [n]
     const uint32_t* heavyBits; // [ceil(n/32)] vertices with degree >= heavyDeg
+    const int32_t* oldId;      // [n] device id -> caller's vertex id (null: identity).
+                               // The batched path relabels vertices by degree (rows
+                               // keep igraph's incidence order); pred is mapped back
 };
 
 // A table holds the contiguous block of rows [rowStart, rowStart + rows) of
@@ -75,10 +78,11 @@ struct Tuning {
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0;
     int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 1, batchWpe = 0;
+    int relabel = 1;           // batched path: 1 = device ids by descending degree, 0 = as given
     double batchDeltaFactor = 1.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
-    int debug = 0, streamWgPerCU = 4;
+    int debug = 0, streamWgPerCU = 16;
 };
 
 struct DevScratch {

@@ -47,6 +47,7 @@ __device__ __forceinline__ DevGraph global_view(const DevGraph& g0) {
     g.attached = as_global(g0.attached);
     g.isAttached = as_global(g0.isAttached);
     g.heavyBits = as_global(g0.heavyBits);
+    g.oldId = g0.oldId ? as_global(g0.oldId) : nullptr;
     return g;
 }
 

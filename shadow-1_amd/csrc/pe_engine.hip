@@ -51,7 +51,8 @@ struct Shard {
     hipStream_t copyStream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evA = nullptr, evB = nullptr;
     std::vector<void*> allocs;
-    DevGraph dg{};
+    DevGraph dg{};                  // path kernels (device ids, possibly relabelled)
+    DevGraph dgAux{};               // caller's ids, rows sorted by id (aux kernels)
     DevTable tab{};                 // this shard's rows
     DevScratch sc{};
     bool tableReady = false;
@@ -151,6 +152,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_GRID", t.batchGrid);
     gi("SHDPE_BATCH_ORDER", t.batchOrder);
     gi("SHDPE_BATCH_WPE", t.batchWpe);
+    gi("SHDPE_RELABEL", t.relabel);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -419,6 +421,138 @@ static void destroy_shard(Shard* s) {
     if (s->copyStream) (void)hipStreamDestroy(s->copyStream);
 }
 
+// Upload the graph as a DevGraph.  oldOf == null: the caller's vertex ids.
+// Otherwise device id k is the caller's vertex oldOf[k]: per-vertex arrays
+// are permuted and arc targets renamed, but every row keeps its arcs in
+// igraph incidence order (ascending CALLER id), so every pop / push order --
+// and the tie-breaking that depends on it -- is unchanged; kernels map pred
+// back through DevGraph::oldId.
+static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<int32_t>* oldOf) {
+    const HostGraph& g0 = pe->hg;
+    const int32_t n = g0.n;
+    const int64_t m = g0.nArcs();
+    int rc;
+    // permuted host copies (only when relabelling)
+    std::vector<int32_t> newOf, rp, ip;
+    hvec<int32_t> col, o2i, icol;
+    hvec<double> lat, rel, ilat, irel;
+    std::vector<double> vrel, sl, sr;
+    std::vector<uint8_t> hs;
+    std::vector<int32_t> att;
+    const bool perm = oldOf != nullptr;
+    if (perm) {
+        const std::vector<int32_t>& od = *oldOf;
+        newOf.assign(n, 0);
+        for (int32_t k = 0; k < n; ++k) newOf[od[k]] = k;
+        rp.assign(n + 1, 0);
+        for (int32_t k = 0; k < n; ++k) rp[k + 1] = rp[k] + (g0.rowPtr[od[k] + 1] - g0.rowPtr[od[k]]);
+        std::vector<int32_t> arcNew(m);
+        col.resize(m); lat.resize(m); rel.resize(m); o2i.resize(m);
+        for (int32_t k = 0; k < n; ++k) {
+            const int32_t u = od[k];
+            for (int32_t a = g0.rowPtr[u], j = rp[k]; a < g0.rowPtr[u + 1]; ++a, ++j) {
+                arcNew[a] = j;
+                col[j] = newOf[g0.col[a]];
+                lat[j] = g0.lat[a];
+                rel[j] = g0.rel[a];
+            }
+        }
+        if (g0.directed) {
+            ip.assign(n + 1, 0);
+            for (int32_t k = 0; k < n; ++k) ip[k + 1] = ip[k] + (g0.inPtr[od[k] + 1] - g0.inPtr[od[k]]);
+            std::vector<int32_t> inNew(m);
+            icol.resize(m); ilat.resize(m); irel.resize(m);
+            for (int32_t k = 0; k < n; ++k) {
+                const int32_t v = od[k];
+                for (int32_t a = g0.inPtr[v], j = ip[k]; a < g0.inPtr[v + 1]; ++a, ++j) {
+                    inNew[a] = j;
+                    icol[j] = newOf[g0.inCol[a]];
+                    ilat[j] = g0.inLat[a];
+                    irel[j] = g0.inRel[a];
+                }
+            }
+            for (int64_t a = 0; a < m; ++a) o2i[arcNew[a]] = inNew[g0.outToIn[a]];
+        } else {
+            for (int64_t a = 0; a < m; ++a) o2i[arcNew[a]] = arcNew[g0.outToIn[a]];
+        }
+        vrel.resize(n); sl.resize(n); sr.resize(n); hs.resize(n);
+        for (int32_t k = 0; k < n; ++k) {
+            vrel[k] = g0.vrel[od[k]]; sl[k] = g0.selfLat[od[k]];
+            sr[k] = g0.selfRel[od[k]]; hs[k] = g0.hasSelf[od[k]];
+        }
+        att.resize(pe->attached.size());
+        for (size_t i = 0; i < att.size(); ++i) att[i] = newOf[pe->attached[i]];
+    }
+    const std::vector<int32_t>& RP = perm ? rp : g0.rowPtr;
+    const hvec<int32_t>& COL = perm ? col : g0.col;
+    const hvec<double>& LAT = perm ? lat : g0.lat;
+    const hvec<double>& REL = perm ? rel : g0.rel;
+    const std::vector<int32_t>& ATT = perm ? att : pe->attached;
+    DevGraph d{};
+    d.n = n;
+    d.T = (int32_t)pe->attached.size();
+    std::vector<uint8_t> isAtt(n, 0);
+    for (int32_t v : ATT) isAtt[v] = 1;
+    int32_t *rowPtr, *dcol, *outToIn, *datt;
+    double *dlat, *drel, *dvrel, *dsl, *dsr;
+    uint8_t *dhs, *ia;
+    if ((rc = dev_upload(sh, &rowPtr, RP)) || (rc = dev_upload(sh, &dcol, COL)) ||
+        (rc = dev_upload(sh, &dlat, LAT)) || (rc = dev_upload(sh, &drel, REL)) ||
+        (rc = dev_upload(sh, &outToIn, perm ? o2i : g0.outToIn)) ||
+        (rc = dev_upload(sh, &dvrel, perm ? vrel : g0.vrel)) ||
+        (rc = dev_upload(sh, &dsl, perm ? sl : g0.selfLat)) ||
+        (rc = dev_upload(sh, &dsr, perm ? sr : g0.selfRel)) ||
+        (rc = dev_upload(sh, &dhs, perm ? hs : g0.hasSelf)) || (rc = dev_upload(sh, &datt, ATT)) ||
+        (rc = dev_upload(sh, &ia, isAtt)))
+        return rc;
+    {
+        std::vector<Arc> arcs(COL.size());
+        for (size_t a = 0; a < arcs.size(); ++a) arcs[a] = Arc{LAT[a], COL[a], 0};
+        Arc* da;
+        if ((rc = dev_upload(sh, &da, arcs))) return rc;
+        d.arcs = da;
+        std::vector<Arc3> a3(COL.size());
+        for (size_t a = 0; a < a3.size(); ++a) {
+            uint64_t bits;
+            std::memcpy(&bits, &LAT[a], 8);
+            a3[a] = Arc3{COL[a], (uint32_t)bits, (uint32_t)(bits >> 32)};
+        }
+        Arc3* d3;
+        if ((rc = dev_upload(sh, &d3, a3))) return rc;
+        d.arc3 = d3;
+    }
+    d.rowPtr = rowPtr; d.col = dcol; d.lat = dlat; d.rel = drel; d.outToIn = outToIn;
+    d.vrel = dvrel; d.selfLat = dsl; d.selfRel = dsr; d.hasSelf = dhs; d.attached = datt;
+    d.isAttached = ia;
+    {
+        const int hd = sh->cfg.heavyDeg;
+        std::vector<uint32_t> hb((n + 31) / 32, 0u);
+        for (int32_t v = 0; v < n; ++v)
+            if (RP[v + 1] - RP[v] >= hd) hb[v >> 5] |= 1u << (v & 31);
+        uint32_t* dhb;
+        if ((rc = dev_upload(sh, &dhb, hb))) return rc;
+        d.heavyBits = dhb;
+    }
+    if (g0.directed) {
+        int32_t *dip, *dic;
+        double *dil, *dir;
+        if ((rc = dev_upload(sh, &dip, perm ? ip : g0.inPtr)) || (rc = dev_upload(sh, &dic, perm ? icol : g0.inCol)) ||
+            (rc = dev_upload(sh, &dil, perm ? ilat : g0.inLat)) || (rc = dev_upload(sh, &dir, perm ? irel : g0.inRel)))
+            return rc;
+        d.inPtr = dip; d.inCol = dic; d.inLat = dil; d.inRel = dir;
+    } else {
+        d.inPtr = rowPtr; d.inCol = dcol; d.inLat = dlat; d.inRel = drel;
+    }
+    d.oldId = nullptr;
+    if (perm) {
+        int32_t* dold;
+        if ((rc = dev_upload(sh, &dold, *oldOf))) return rc;
+        d.oldId = dold;
+    }
+    *out = d;
+    return SHD_PE_OK;
+}
+
 // Device state of one shard: graph upload, stream, events, kernel config.
 static int init_shard(ShdPe* pe, Shard* sh) {
     const HostGraph& g = pe->hg;
@@ -435,58 +569,19 @@ static int init_shard(ShdPe* pe, Shard* sh) {
     int rc = configure(pe, sh);
     if (rc) return rc;
     const int32_t T = (int32_t)pe->attached.size();
-    DevGraph& d = sh->dg;
-    d.n = g.n;
-    d.T = T;
-    std::vector<uint8_t> isAtt(g.n, 0);
-    for (int32_t v : pe->attached) isAtt[v] = 1;
-    int32_t *rowPtr, *col, *outToIn, *att;
-    double *lat, *rel, *vrel, *sl, *sr;
-    uint8_t *hs, *ia;
-    if ((rc = dev_upload(sh, &rowPtr, g.rowPtr)) || (rc = dev_upload(sh, &col, g.col)) ||
-        (rc = dev_upload(sh, &lat, g.lat)) || (rc = dev_upload(sh, &rel, g.rel)) ||
-        (rc = dev_upload(sh, &outToIn, g.outToIn)) || (rc = dev_upload(sh, &vrel, g.vrel)) ||
-        (rc = dev_upload(sh, &sl, g.selfLat)) || (rc = dev_upload(sh, &sr, g.selfRel)) ||
-        (rc = dev_upload(sh, &hs, g.hasSelf)) || (rc = dev_upload(sh, &att, pe->attached)) ||
-        (rc = dev_upload(sh, &ia, isAtt)))
-        return rc;
-    {
-        std::vector<Arc> arcs(g.col.size());
-        for (size_t a = 0; a < arcs.size(); ++a) arcs[a] = Arc{g.lat[a], g.col[a], 0};
-        Arc* da;
-        if ((rc = dev_upload(sh, &da, arcs))) return rc;
-        d.arcs = da;
-        std::vector<Arc3> a3(g.col.size());
-        for (size_t a = 0; a < a3.size(); ++a) {
-            uint64_t bits;
-            std::memcpy(&bits, &g.lat[a], 8);
-            a3[a] = Arc3{g.col[a], (uint32_t)bits, (uint32_t)(bits >> 32)};
-        }
-        Arc3* d3;
-        if ((rc = dev_upload(sh, &d3, a3))) return rc;
-        d.arc3 = d3;
-    }
-    d.rowPtr = rowPtr; d.col = col; d.lat = lat; d.rel = rel; d.outToIn = outToIn;
-    d.vrel = vrel; d.selfLat = sl; d.selfRel = sr; d.hasSelf = hs; d.attached = att;
-    d.isAttached = ia;
-    {
-        const int hd = sh->cfg.heavyDeg;
-        std::vector<uint32_t> hb((g.n + 31) / 32, 0u);
-        for (int32_t v = 0; v < g.n; ++v)
-            if (g.rowPtr[v + 1] - g.rowPtr[v] >= hd) hb[v >> 5] |= 1u << (v & 31);
-        uint32_t* dhb;
-        if ((rc = dev_upload(sh, &dhb, hb))) return rc;
-        d.heavyBits = dhb;
-    }
-    if (g.directed) {
-        int32_t *ip, *ic;
-        double *il, *ir;
-        if ((rc = dev_upload(sh, &ip, g.inPtr)) || (rc = dev_upload(sh, &ic, g.inCol)) ||
-            (rc = dev_upload(sh, &il, g.inLat)) || (rc = dev_upload(sh, &ir, g.inRel)))
-            return rc;
-        d.inPtr = ip; d.inCol = ic; d.inLat = il; d.inRel = ir;
-    } else {
-        d.inPtr = rowPtr; d.inCol = col; d.inLat = lat; d.inRel = rel;
+    if ((rc = upload_graph(pe, sh, &sh->dgAux, nullptr))) return rc;
+    sh->dg = sh->dgAux;
+    if (pe->batched && pe->tu.relabel == 1) {
+        // device ids by descending degree (stable): a wave's groups get
+        // vertices of similar degree in the queue and predecessor pass (less
+        // divergence), and the hubs' [v][LB] lines sit together
+        const int32_t n = g.n;
+        std::vector<int32_t> oldOf(n);
+        for (int32_t v = 0; v < n; ++v) oldOf[v] = v;
+        std::stable_sort(oldOf.begin(), oldOf.end(), [&](int32_t a, int32_t b) {
+            return g.rowPtr[a + 1] - g.rowPtr[a] > g.rowPtr[b + 1] - g.rowPtr[b];
+        });
+        if ((rc = upload_graph(pe, sh, &sh->dg, &oldOf))) return rc;
     }
     sh->stats.mode = pe->mode;
     sh->stats.isComplete = g.isComplete ? 1 : 0;
@@ -1440,22 +1535,26 @@ extern "C" int shd_pe_owned_range(const ShdPe* pe, int32_t* start, int32_t* coun
 }
 
 // Streaming copy for the achievable-HBM reference: 16-B
-// loads and stores, grid-stride, enough workgroups to fill all 8 XCDs.
+// loads and stores (float4-shaped), each thread moving UNR consecutive-stride
+// elements per iteration so UNR loads are in flight before the first store,
+// grid-stride over a footprint far past the 256 MiB Infinity Cache.  The
+// reference is the best of a few shapes (cache policy x workgroups per CU):
+// the figure is what this box's HBM delivers to a well-formed copy.
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+template <bool NT, int UNR>
 __global__ __launch_bounds__(256) void k_stream_copy(const v4u* __restrict__ a,
                                                       v4u* __restrict__ b, size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        // non-temporal: the copy streams through, nothing is re-read
-        const v4u x0 = __builtin_nontemporal_load(&a[i]);
-        const v4u x1 = __builtin_nontemporal_load(&a[i + stride]);
-        const v4u x2 = __builtin_nontemporal_load(&a[i + 2 * stride]);
-        const v4u x3 = __builtin_nontemporal_load(&a[i + 3 * stride]);
-        __builtin_nontemporal_store(x0, &b[i]);
-        __builtin_nontemporal_store(x1, &b[i + stride]);
-        __builtin_nontemporal_store(x2, &b[i + 2 * stride]);
-        __builtin_nontemporal_store(x3, &b[i + 3 * stride]);
+    for (; i + (UNR - 1) * stride < n; i += UNR * stride) {
+        v4u x[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) x[k] = NT ? __builtin_nontemporal_load(&a[i + k * stride]) : a[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            if (NT) __builtin_nontemporal_store(x[k], &b[i + k * stride]);
+            else b[i + k * stride] = x[k];
+        }
     }
     for (; i < n; i += stride) b[i] = a[i];
 }
@@ -1469,24 +1568,36 @@ extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, 
     if (hipMalloc(&a, n * 16) != hipSuccess) return SHD_PE_ENOMEM;
     if (hipMalloc(&b, n * 16) != hipSuccess) { (void)hipFree(a); return SHD_PE_ENOMEM; }
     int rc = SHD_PE_OK;
-    const int grid = sh->numCUs * pe->tu.streamWgPerCU;
+    double best = 0.0;
     if (hipMemsetAsync(a, 0, n * 16, sh->stream) != hipSuccess) rc = SHD_PE_EHIP;
-    if (!rc) {
-        hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, sh->stream, (const v4u*)a,
-                           (v4u*)b, n);   // warm-up
+    // shapes: cache policy (plain / non-temporal) x 4 or 8 loads in flight per
+    // thread x workgroups per CU (SHDPE_STREAM_WG_PER_CU adds one more)
+    const int wgs[3] = {4, 8, pe->tu.streamWgPerCU};
+    for (int shape = 0; shape < 12 && !rc; ++shape) {
+        const bool nt = shape & 1;
+        const int unr = (shape >> 1) & 1 ? 8 : 4;
+        const int grid = sh->numCUs * wgs[shape >> 2];
+        auto launch = [&]() {
+            const v4u* pa = (const v4u*)a;
+            v4u* pb = (v4u*)b;
+            if (nt && unr == 8) hipLaunchKernelGGL((k_stream_copy<true, 8>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+            else if (nt) hipLaunchKernelGGL((k_stream_copy<true, 4>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+            else if (unr == 8) hipLaunchKernelGGL((k_stream_copy<false, 8>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+            else hipLaunchKernelGGL((k_stream_copy<false, 4>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+        };
+        launch();   // warm-up
         (void)hipEventRecord(sh->evA, sh->stream);
-        for (int i = 0; i < iters; ++i)
-            hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, sh->stream,
-                               (const v4u*)a, (v4u*)b, n);
+        for (int i = 0; i < iters; ++i) launch();
         (void)hipEventRecord(sh->evB, sh->stream);
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(sh->stream) != hipSuccess)
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(sh->stream) != hipSuccess) {
             rc = SHD_PE_EHIP;
-    }
-    if (!rc) {
+            break;
+        }
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, sh->evA, sh->evB);
-        *gbps = ms > 0.f ? 2.0 * (double)n * 16.0 * iters / (ms * 1e-3) / 1e9 : 0.0;
+        if (ms > 0.f) best = std::max(best, 2.0 * (double)n * 16.0 * iters / (ms * 1e-3) / 1e9);
     }
+    if (!rc) *gbps = best;
     (void)hipFree(a);
     (void)hipFree(b);
     return rc;
@@ -1614,7 +1725,7 @@ extern "C" int shd_pe_self_paths(ShdPe* pe, const int32_t* vertices, int32_t cou
     for (int64_t c0 = 0; c0 < count; c0 += ch) {
         const int32_t c = (int32_t)std::min<int64_t>(ch, count - c0);
         HIPCHK(hipMemcpyAsync(b.p[0], vertices + c0, (size_t)c * 4, hipMemcpyHostToDevice, sh->stream));
-        launch_self_paths(sh->dg, (const int32_t*)b.p[0], c, pe->hg.nEdges, (double*)b.p[1],
+        launch_self_paths(sh->dgAux, (const int32_t*)b.p[0], c, pe->hg.nEdges, (double*)b.p[1],
                           (double*)b.p[2], (uint8_t*)b.p[3], sh->stream);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(lat + c0, b.p[1], (size_t)c * 8, hipMemcpyDeviceToHost, sh->stream));
@@ -1642,7 +1753,7 @@ static int pairs_call(ShdPe* pe, const int32_t* src, const int32_t* dst, int64_t
         const int64_t c = std::min<int64_t>(ch, count - c0);
         HIPCHK(hipMemcpyAsync(b.p[0], src + c0, (size_t)c * 4, hipMemcpyHostToDevice, sh->stream));
         HIPCHK(hipMemcpyAsync(b.p[1], dst + c0, (size_t)c * 4, hipMemcpyHostToDevice, sh->stream));
-        launch_pairs(sh->dg, (const int32_t*)b.p[0], (const int32_t*)b.p[1], c, mode,
+        launch_pairs(sh->dgAux, (const int32_t*)b.p[0], (const int32_t*)b.p[1], c, mode,
                      (double*)b.p[2], (double*)b.p[3], (uint8_t*)b.p[4], sh->stream);
         HIPCHK(hipGetLastError());
         if (mode == 0) {
@@ -1674,7 +1785,7 @@ extern "C" int shd_pe_is_complete_device(ShdPe* pe, int32_t* isComplete) {
     if (hipMalloc(&b.p[0], 4)) return SHD_PE_ENOMEM;
     const int32_t init = INT32_MAX;
     HIPCHK(hipMemcpyAsync(b.p[0], &init, 4, hipMemcpyHostToDevice, sh->stream));
-    launch_incident_min(sh->dg, (int32_t*)b.p[0], sh->stream);
+    launch_incident_min(sh->dgAux, (int32_t*)b.p[0], sh->stream);
     HIPCHK(hipGetLastError());
     int32_t mn = 0;
     HIPCHK(hipMemcpyAsync(&mn, b.p[0], 4, hipMemcpyDeviceToHost, sh->stream));

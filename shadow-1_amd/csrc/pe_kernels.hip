@@ -155,7 +155,10 @@ __device__ __forceinline__ void write_row(const DevGraph& g, const DevTable& tab
             } else {
                 L = b2d(db[k]);
                 h = hh[k];
-                if (oPred) pv = g.inCol[pa[k]];
+                if (oPred) {
+                    pv = g.inCol[pa[k]];
+                    if (g.oldId) pv = g.oldId[pv];      // device id -> caller's id
+                }
                 if (g.vrel[s] == 1.0 && g.vrel[t] == 1.0) Rl = rr[k];
                 else Rl = fold_rel_general(g.vrel, g.inRel, g.inCol, P, s, t, h);
                 if (L == 0.0) {                    // topology.c:1848-1852

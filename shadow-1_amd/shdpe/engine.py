@@ -163,6 +163,21 @@ def plan_shards(T: int, G: int, unit: int = 1) -> np.ndarray:
     return b
 
 
+def kernel_source_hash() -> str:
+    """sha256 (first 16 hex digits) of the device-code sources libshdpe.so is
+    built from (csrc/*.hip, *.hpp): identifies the measured kernels in
+    profiles/traffic_<wl>.json so bench.py drops a stale traffic figure."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(_PKG, "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def strerror(code: int) -> str:
     return load_library().shd_pe_strerror(int(code)).decode()
 

@@ -35,6 +35,21 @@ for st in ${STAGES:-tests bench}; do
   debug)
     SHDPE_DEBUG=1 timeout -k 10 300 python3 -u bench.py --workload ${DEBUG_WL:-c4} --steps 1 --warmup 0 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $OUT/debug.json 2> $OUT/debug.err || { tail -20 $OUT/debug.err; exit 1; }
     grep shdpe $OUT/debug.err | head -20 ;;
+  pmc)
+    # L2-miss traffic of one launch per workload: FETCH_SIZE / WRITE_SIZE /
+    # TCC hit+miss in separate passes (MI355X_MICROARCH.md HBM section)
+    for wl in ${WLS//,/ }; do
+      for PASS in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" ${EXTRA_PASSES}; do
+        T2=$(echo $PASS | tr ' ' '_' | cut -c1-40)
+        (cd /tmp && TMPDIR=/tmp timeout -s KILL 150 rocprofv3 --pmc $PASS --output-format csv -d $R/$OUT/pmc_${wl}_$T2 -o pmc -- python3 $R/bench.py --workload $wl --steps 1 --warmup 0 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $R/$OUT/pmc_${wl}_$T2.log 2>&1) || { echo "pmc pass $wl $PASS failed"; tail -5 $OUT/pmc_${wl}_$T2.log; exit 1; }
+      done
+      python3 tools/traffic_json.py $OUT $wl $TAG $OUT/traffic_$wl.json || exit 1
+    done ;;
+  trace)
+    for wl in ${WLS//,/ }; do
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace_$wl -o trace -- python3 $R/bench.py --workload $wl --steps 5 --warmup 1 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $R/$OUT/trace_$wl.json 2> $R/$OUT/trace_$wl.err) || { tail -20 $OUT/trace_$wl.err; exit 1; }
+      line $OUT/trace_$wl.json "$wl traced"
+    done ;;
   relabel)
     timeout -k 10 400 python3 -u tools/relabel_probe.py ${RELABEL_WL:-c4} > $OUT/relabel.txt 2>&1 || { tail -20 $OUT/relabel.txt; exit 1; }
     cat $OUT/relabel.txt ;;

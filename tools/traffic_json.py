@@ -1,0 +1,69 @@
+"""Turn one workload's rocprofv3 PMC passes into profiles/traffic_<wl>.json.
+
+usage: python tools/traffic_json.py <pmc outdir> <workload> <tag> [out.json]
+
+Reads the counter_collection CSVs under <outdir>/pmc_<wl>_* (one launch of
+the dominant kernel per pass, bench.py --steps 1 --warmup 0), applies the
+gfx950 FETCH_SIZE correction this kernel shape was calibrated for
+(profiles/r02e_fetch_calibration.json: random 128-B lines read by 16-lane
+groups report half their bytes) and records the kernel-source hash of the
+library that was measured, so bench.py only reports `traffic` for a build
+whose sources match (shdpe.engine.kernel_source_hash).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "shadow-1_amd")]
+
+KERNELS = ("k_batch_rows", "k_sparse_rows", "k_minplus", "k_direct_rows")
+
+
+def main():
+    outdir, wl, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    dst = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles", f"traffic_{wl}.json")
+    tot = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(lambda: defaultdict(set))
+    for f in glob.glob(os.path.join(outdir, f"pmc_{wl}_*", "**", "*counter_collection*.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = next((k for k in KERNELS if k in r.get("Kernel_Name", "")), None)
+            if k is None:
+                continue
+            tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[k][r["Counter_Name"]].add((f, r.get("Dispatch_Id")))
+    if not tot:
+        sys.exit(f"no counters for the path kernels under {outdir}/pmc_{wl}_*")
+    k = max(tot, key=lambda x: tot[x].get("FETCH_SIZE", 0.0))
+    c = tot[k]
+    nl = max(1, len(disp[k].get("FETCH_SIZE", ())))
+    fetch = c.get("FETCH_SIZE", 0.0) * 1024 / nl
+    write = c.get("WRITE_SIZE", 0.0) * 1024 / max(1, len(disp[k].get("WRITE_SIZE", ())))
+    hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
+    from shdpe.engine import kernel_source_hash
+    out = {
+        "kernel": k,
+        "bytes_per_launch": 2 * fetch + write,
+        "read_bytes": 2 * fetch,
+        "fetch_size_bytes": fetch,
+        "write_bytes": write,
+        "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
+        "launches_per_pass": nl,
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, KB*1024, "
+                  "bench.py --steps 1 --warmup 0 (one launch).  Reads = 2 x FETCH_SIZE (gfx950 "
+                  "calibration for random 128-B lines, profiles/r02e_fetch_calibration.json); "
+                  "writes = WRITE_SIZE.  L2-miss traffic (includes Infinity-Cache hits): an upper "
+                  "bound on HBM bytes.",
+        "tag": tag,
+        "src_hash": kernel_source_hash(),
+    }
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
