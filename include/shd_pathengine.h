@@ -50,8 +50,9 @@ extern "C" {
 #define SHD_PE_ENOTATTACHED -8   /* vertex is not in the attached set              */
 #define SHD_PE_ENOEDGE      -9   /* direct path requested but (s,t) has no edge    */
 #define SHD_PE_ENOTOWNED   -10   /* row lives in another engine's shard (gather)   */
-#define SHD_PE_ETOOBIG     -11   /* graph exceeds the LDS-resident frontier limit
-                                    (about 520,000 vertices)                       */
+#define SHD_PE_ETOOBIG     -11   /* graph exceeds the engine's kernel limits (int32
+                                    arc / entry indices; no vertex-count cap since
+                                    the pending bitmaps spill to HBM past ~655k)   */
 #define SHD_PE_ECOMM       -12   /* RCCL communicator missing or failed            */
 
 /* ---- per-entry flags (uint8) ------------------------------------------ */
@@ -181,13 +182,21 @@ int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double* rel,
 /* Bulk copy of table rows by position [start, start+count) into caller
  * buffers laid out row-major (count x T, attached order), same fields and
  * values as shd_pe_get_row; any pointer may be NULL.  Rows not yet computed
- * are computed first.  The copy streams through the engine's pinned staging
- * buffers (DMA of the next block overlaps the host copy of the current one),
- * so a host row store filled after shd_pe_compute_all (topology.c's cache
- * inserts, :1805-1864) pays one pass at PCIe rate instead of one
- * synchronous transfer per field per row. */
+ * are computed first.  Buffers from shd_pe_host_alloc (or otherwise
+ * page-locked) receive the DMA directly; pageable buffers are filled through
+ * the engine's pinned staging buffers (DMA of the next block overlaps the
+ * multi-threaded host copy of the current one).  Either way a host row store
+ * filled after shd_pe_compute_all (topology.c's cache inserts, :1805-1864)
+ * pays one pass at PCIe rate instead of one synchronous transfer per field
+ * per row. */
 int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
                     int32_t* hops, int32_t* pred, uint8_t* flags);
+
+/* Page-locked host memory for shd_pe_get_rows destinations (DMA target, no
+ * staging copy).  No reference counterpart: Shadow's row buffers are plain
+ * g_new allocations (topology.c:1805-1864). */
+int shd_pe_host_alloc(int64_t bytes, void** out);
+void shd_pe_host_free(void* p);
 
 /* Copy rows [start, start+count) (table positions) of the device table into
  * caller DEVICE buffers (e.g. an RCCL all-gather staging area).  Row-major,

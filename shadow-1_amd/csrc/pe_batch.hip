@@ -77,11 +77,62 @@ __device__ __forceinline__ unsigned long long enc_dirty(unsigned long long bits)
 __device__ __forceinline__ unsigned long long dec(unsigned long long e) { return e >> 1; }
 constexpr unsigned long long INF_ENC = (INF_BITS << 1) | 1ull;
 
+// (A/B experiment knobs, see tools/build_variant.sh)
+__device__ __forceinline__ void relax_min(unsigned long long* p, unsigned long long v) {
+#ifdef SHDPE_X_PLAIN_RELAX
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef SHDPE_X_DOUBLE_ATOMIC
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+#endif
+}
+
+// relax pre-check load (A/B knob: SHDPE_X_DOUBLE_READ also reads the line of
+// the vertex 96 ids lower, same lane: the cost of one more random line read
+// per arc visit)
+__device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, int x, int LB, int l) {
+#ifdef SHDPE_X_DOUBLE_READ
+    const unsigned long long a = ld_wg(&D[(size_t)x * LB + l]);
+    const int y = x >= 96 ? x - 96 : x;
+    const unsigned long long b = ld_wg(&D[(size_t)y * LB + l]);
+    return b == 12345ull ? b : a;
+#else
+    return ld_wg(&D[(size_t)x * LB + l]);
+#endif
+}
+
 __device__ __forceinline__ void mark_clean(unsigned long long* p, unsigned long long e) {
+#ifdef SHDPE_X_PLAIN_CLEAN
+    __hip_atomic_store(p, e | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+#endif
     unsigned long long expect = e;
     (void)__hip_atomic_compare_exchange_strong(p, &expect, e | 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
+// Pending bitmaps (one bit per vertex, near + far sets): in LDS when both
+// fit beside the control block (n <= ~655k), else in the slot's global
+// scratch (GB): same operations at workgroup scope.
+template <bool GB> struct Bits;
+template <> struct Bits<false> {
+    uint32_t* p;
+    __device__ __forceinline__ uint32_t ld(int w) const { return p[w]; }
+    __device__ __forceinline__ void st(int w, uint32_t v) const { p[w] = v; }
+    __device__ __forceinline__ void set(int v) const { atomicOr(&p[v >> 5], 1u << (v & 31)); }
+};
+template <> struct Bits<true> {
+    uint32_t* p;
+    __device__ __forceinline__ uint32_t ld(int w) const { return ld_wg(&p[w]); }
+    __device__ __forceinline__ void st(int w, uint32_t v) const {
+        __hip_atomic_store(&p[w], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void set(int v) const {
+        __hip_atomic_fetch_or(&p[v >> 5], 1u << (v & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+};
 
 // bucket of a key: the smallest multiple of delta above it
 __device__ __forceinline__ double next_bound(double mn, double delta) {
@@ -125,7 +176,7 @@ __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
     return acc;
 }
 
-template <int LB, int WPE>
+template <int LB, int WPE, bool GB>
 __global__ __launch_bounds__(BT_THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_batch_rows(DevGraph g0, DevTable tab0,
                                                            BatchScratch bs,
@@ -152,8 +203,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const size_t NE = (size_t)n * LB;        // (vertex, lane) entries
 
     BCtrl* ctl = reinterpret_cast<BCtrl*>(smem);
-    uint32_t* const any0 = reinterpret_cast<uint32_t*>(smem + 64);
-    uint32_t* const any1 = any0 + nwp;
+    uint32_t* const bits0 = GB ? as_global(bs.bits) + (size_t)blockIdx.x * 2 * nwp
+                               : reinterpret_cast<uint32_t*>(smem + 64);
+    const Bits<GB> any0{bits0}, any1{bits0 + nwp};
 
     const size_t slot = blockIdx.x;
     const size_t NS = (size_t)bs.nStride;
@@ -180,7 +232,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             const size_t cnt2 = NE / 2;
             const ulonglong2 inf2 = make_ulonglong2(INF_ENC, INF_ENC);
             for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
-            for (int w = tid; w < nwp; w += NT) { any0[w] = 0u; any1[w] = 0u; }
+            for (int w = tid; w < nwp; w += NT) { any0.st(w, 0u); any1.st(w, 0u); }
             if (tid == 0) {
                 ctl->qtail = 0;
                 ctl->farAny = 0;
@@ -202,7 +254,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (gid == 0 && src >= 0) {
             D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
             R[(size_t)src * LB + l] = 1.0;
-            atomicOr(&any0[src >> 5], 1u << (src & 31));
+            any0.set(src);
         }
         fence_wg();
         __syncthreads();
@@ -233,16 +285,16 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         unsigned long long myFar = INF_BITS;      // smallest far key this thread added
         for (;;) {   // phases + verification until the Bellman check holds
         for (;;) {
-            uint32_t* const anyC = par ? any1 : any0;   // near
-            uint32_t* const anyF = par ? any0 : any1;   // far
+            const Bits<GB> anyC = par ? any1 : any0;   // near
+            const Bits<GB> anyF = par ? any0 : any1;   // far
             // candidates = vertices with a near bit (consumed)
             // (hubs -- degree >= the engine's heavy threshold -- go to a list
             // of their own, processed by whole waves: one 16-lane group on a
             // hub's ~1000 arcs would set the phase's length)
             for (int w = tid; w < nw; w += NT) {
-                uint32_t bits = anyC[w];
+                uint32_t bits = anyC.ld(w);
                 if (bits) {
-                    anyC[w] = 0u;
+                    anyC.st(w, 0u);
                     uint32_t hv = bits & g.heavyBits[w];
                     bits &= ~hv;
                     if (bits) {
@@ -309,7 +361,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const bool defer = dirty && !(k0 < bound);
                     const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
                     const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                    if (gw == 0 && l == 0 && dmask) atomicOr(&anyF[u >> 5], 1u << (u & 31));
+                    if (gw == 0 && l == 0 && dmask) anyF.set(u);
                     if (gw == 0 && defer) {
                         myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
                         farAdd = 1;
@@ -336,7 +388,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[k] = ld_wg(&D[(size_t)(xs[k] >= 0 ? xs[k] : 0) * LB + l]);
+                            dx[k] = relax_ld(D, xs[k] >= 0 ? xs[k] : 0, LB, l);
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const int x = xs[k];
@@ -345,8 +397,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 const double nd = b2d(dub1) + ws[k];
                                 const unsigned long long nb = d2b(nd);
                                 if (nb < dec(dx[k])) {
-                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], enc_dirty(nb), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    relax_min(&D[(size_t)x * LB + l], enc_dirty(nb));
                                     const double kx = nd + sh;
                                     impN = kx < bound;
                                     impF = !impN;
@@ -355,9 +406,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             }
                             const uint64_t bn = __ballot(impN), bf = __ballot(impF);
                             if (l == 0) {
-                                if ((bn >> gbase) & LBMASK) atomicOr(&anyC[x >> 5], 1u << (x & 31));
+                                if ((bn >> gbase) & LBMASK) anyC.set(x);
                                 if ((bf >> gbase) & LBMASK) {
-                                    atomicOr(&anyF[x >> 5], 1u << (x & 31));
+                                    anyF.set(x);
                                     farAdd = 1;
                                 }
                             }
@@ -403,7 +454,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const bool defer = dirty && !(k0 < bound);
                     const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
                     const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                    if (l == 0 && dmask) atomicOr(&anyF[u[v] >> 5], 1u << (u[v] & 31));
+                    if (l == 0 && dmask) anyF.set(u[v]);
                     if (defer) {
                         myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
                         farAdd = 1;
@@ -440,7 +491,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[v][k] = ld_wg(&D[(size_t)(xs[v][k] >= 0 ? xs[v][k] : 0) * LB + l]);
+                            dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l);
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
@@ -451,8 +502,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 const double nd = b2d(dub[v]) + ws[v][k];
                                 const unsigned long long nb = d2b(nd);
                                 if (nb < dec(dx[v][k])) {
-                                    __hip_atomic_fetch_min(&D[(size_t)x * LB + l], enc_dirty(nb), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    relax_min(&D[(size_t)x * LB + l], enc_dirty(nb));
                                     const double kx = nd + sh;
                                     impN = kx < bound;
                                     impF = !impN;
@@ -461,9 +511,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             }
                             const uint64_t bn = __ballot(impN), bf = __ballot(impF);
                             if (l == 0) {
-                                if ((bn >> gbase) & LBMASK) atomicOr(&anyC[x >> 5], 1u << (x & 31));
+                                if ((bn >> gbase) & LBMASK) anyC.set(x);
                                 if ((bf >> gbase) & LBMASK) {
-                                    atomicOr(&anyF[x >> 5], 1u << (x & 31));
+                                    anyF.set(x);
                                     farAdd = 1;
                                 }
                             }
@@ -504,7 +554,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         //     row (k_exact_rows) if such an entry lies on a target's path.
         int viol = 0;
         {
-            uint32_t* const anyC = par ? any1 : any0;
+            const Bits<GB> anyC = par ? any1 : any0;
             for (int v0 = gid * BV; v0 < n; v0 += NG * BV) {
                 int a0[BV], a1[BV], ba[BV], cnt[BV], bu[BV];
                 unsigned long long dvb[BV], best[BV], mn[BV];
@@ -591,7 +641,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         viol = 1;
                     }
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
-                    if (bm && l == 0) atomicOr(&anyC[vv >> 5], 1u << (vv & 31));
+                    if (bm && l == 0) anyC.set(vv);
                     const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
                     // an entry whose parent the heap decides: equal minimum
                     // tight predecessors, or the minimum one reaches v by a
@@ -880,43 +930,51 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     }
 }
 
-template <int LB, int WPE>
+template <int LB, int WPE, bool GB>
 static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st,
                       int grid) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB, WPE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB, WPE, GB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-    hipLaunchKernelGGL((k_batch_rows<LB, WPE>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
+    hipLaunchKernelGGL((k_batch_rows<LB, WPE, GB>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
                        bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
 }
 
-int batch_lds_bytes(int n, int wpe) {
+int batch_lds_bytes(int n, int wpe, bool gbits) {
     const int nwp = (((n + 31) >> 5) + 3) & ~3;
     // label walks reuse the relax bitmaps' LDS for their stacks
     const int stack = BT_THREADS * (wpe >= 8 ? BCfg<8>::SMAX : BCfg<4>::SMAX) * 8;
-    return 64 + (2 * 4 * nwp > stack ? 2 * 4 * nwp : stack);
+    const int bits = gbits ? 0 : 2 * 4 * nwp;
+    return 64 + (bits > stack ? bits : stack);
 }
+
+int64_t batch_bits_words(int n) { return 2 * (int64_t)((((n + 31) >> 5) + 3) & ~3); }
 
 template <int WPE>
-static const void* kptr(int lb) {
-    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8, WPE>);
-    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32, WPE>);
-    return reinterpret_cast<const void*>(&k_batch_rows<16, WPE>);
+static const void* kptr(int lb, bool gb) {
+    if (gb) return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, true>);
+    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8, WPE, false>);
+    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32, WPE, false>);
+    return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, false>);
 }
 
-const void* batch_kernel_ptr(int lb, int wpe) { return wpe >= 8 ? kptr<8>(lb) : kptr<4>(lb); }
+const void* batch_kernel_ptr(int lb, int wpe, bool gbits) {
+    return wpe >= 8 ? kptr<8>(lb, gbits) : kptr<4>(lb, gbits);
+}
 
 template <int WPE>
 static void launch_w(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                      const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                      const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid) {
-    if (cfg.lb == 8)
-        launch_lb<8, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    if (cfg.gbits)    // graphs whose bitmaps exceed LDS: LB 16 only (the engine forces it)
+        launch_lb<16, WPE, true>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    else if (cfg.lb == 8)
+        launch_lb<8, WPE, false>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (cfg.lb == 32)
-        launch_lb<32, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_lb<32, WPE, false>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else
-        launch_lb<16, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_lb<16, WPE, false>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
 }
 
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,

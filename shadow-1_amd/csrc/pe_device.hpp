@@ -110,6 +110,7 @@ struct BatchScratch {
     int32_t* queue;          // [slot][nStride] phase candidate list
     int32_t* next;           // next batch to take (device counter, zeroed per launch)
     int64_t nStride;         // >= n, multiple of 64
+    uint32_t* bits;          // [slot][2 * words] pending bitmaps when they exceed LDS (gbits)
     const double* rowOff;    // [T] per table position: the source's distance to its
                              // batch hub (bucket key offset; null = no offsets)
 };
@@ -121,6 +122,7 @@ struct BatchLaunch {
     int32_t ldsBytes;
     int32_t wpe;             // waves per SIMD the kernel variant is built for (4 or 8)
     double delta;            // bucket width
+    int32_t gbits;           // 1: pending bitmaps in global scratch (n > ~655k vertices)
 };
 
 // Tie export (pe_batch.hip -> k_exact_rows early stop -> k_tie_write): per
@@ -196,8 +198,9 @@ int sparse_max_threads();
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream);
-const void* batch_kernel_ptr(int lb, int wpe);
-int batch_lds_bytes(int n, int wpe);
+const void* batch_kernel_ptr(int lb, int wpe, bool gbits);
+int batch_lds_bytes(int n, int wpe, bool gbits);
+int64_t batch_bits_words(int n);   // per slot, both bitmaps
 // batched helpers (pe_aux.hip), all on `stream`
 void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, int64_t nEdges,
                        double* dLat, double* dRel, uint8_t* dFlags, void* stream);

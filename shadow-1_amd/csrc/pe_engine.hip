@@ -272,14 +272,18 @@ static int configure(ShdPe* pe, Shard* sh) {
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     // kernel variant: 8 waves per SIMD (two workgroups per CU) when two fit
     // the CU's LDS, else 4 (SHDPE_BATCH_WPE forces one) ...
+    // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
+    // control block, else in each slot's global scratch (gbits, LB 16)
+    b.gbits = pe->batched && batch_lds_bytes((int)n, 8, false) > LDS ? 1 : 0;
+    if (b.gbits) b.lb = 16;
     auto occupancy = [&](int wpe) {
-        const int lds = batch_lds_bytes((int)n, wpe);
+        const int lds = batch_lds_bytes((int)n, wpe, b.gbits != 0);
         int per = 0;
         if (lds > LDS ||
-            hipFuncSetAttribute(batch_kernel_ptr(b.lb, wpe), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                lds) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, batch_kernel_ptr(b.lb, wpe), b.threads,
-                                                         lds) != hipSuccess)
+            hipFuncSetAttribute(batch_kernel_ptr(b.lb, wpe, b.gbits != 0),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, batch_kernel_ptr(b.lb, wpe, b.gbits != 0),
+                                                         b.threads, lds) != hipSuccess)
             per = 0;
         return per;
     };
@@ -289,7 +293,7 @@ static int configure(ShdPe* pe, Shard* sh) {
     b.wpe = tu.batchWpe == 4 || tu.batchWpe == 8
                 ? tu.batchWpe
                 : (nBatchesAll >= 2LL * sh->numCUs && occupancy(8) >= 2 ? 8 : 4);
-    b.ldsBytes = batch_lds_bytes((int)n, b.wpe);
+    b.ldsBytes = batch_lds_bytes((int)n, b.wpe, b.gbits != 0);
     if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
     int bPerCU = b.ldsBytes <= LDS ? occupancy(b.wpe) : 1;
@@ -770,7 +774,8 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     if (sh->batchReady) return SHD_PE_OK;
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     const size_t LB = (size_t)sh->bcfg.lb;
-    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4) + NS * 4;
+    const size_t bitBytes = sh->bcfg.gbits ? (size_t)batch_bits_words(pe->hg.n) * 4 : 0;
+    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4) + NS * 4 + bitBytes;
     // scratch budget (default 64 GiB): fewer resident batches on huge graphs
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
@@ -792,6 +797,12 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bsc.queue = (int32_t*)q;
     sh->bsc.next = (int32_t*)q + slots * NS;
     sh->bsc.nStride = (int64_t)NS;
+    sh->bsc.bits = nullptr;
+    if (bitBytes) {
+        void* bits;
+        if ((rc = dev_alloc(sh, &bits, slots * bitBytes))) return rc;
+        sh->bsc.bits = (uint32_t*)bits;
+    }
     sh->bsc.rowOff = nullptr;
     if (!pe->rowOff.empty()) {
         double* ro;
@@ -1231,9 +1242,41 @@ extern "C" int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double*
     return get_rows_staged(pe, p, 1, lat, rel, hops, pred, flags);
 }
 
-// Rows [start, start+count) -> caller host buffers through two pinned
-// staging buffers: block b's five field copies run on the copy stream while
-// the host copies block b-1 out of the other buffer.
+// Host memcpy split over up to 8 threads: the drain of a staging block into
+// caller (pageable, often freshly allocated) memory runs at one core's
+// page-fault + copy rate otherwise.
+static void par_memcpy(void* dst, const void* src, size_t bytes) {
+    const size_t minChunk = (size_t)2 << 20;
+    const unsigned hc = std::thread::hardware_concurrency();
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>({(size_t)8, hc ? hc : 1, bytes / minChunk}));
+    if (nt <= 1) { std::memcpy(dst, src, bytes); return; }
+    std::vector<std::thread> th;
+    const size_t per = (bytes + nt - 1) / nt;
+    for (int t = 1; t < nt; ++t) {
+        const size_t o = per * t;
+        if (o >= bytes) break;
+        th.emplace_back([=]() { std::memcpy((char*)dst + o, (const char*)src + o, std::min(per, bytes - o)); });
+    }
+    std::memcpy(dst, src, std::min(per, bytes));
+    for (auto& x : th) x.join();
+}
+
+// Page-locked host memory the device can DMA into (hipHostMalloc or
+// hipHostRegister): such caller buffers skip the staging copy.
+static bool is_pinned(const void* p) {
+    if (!p) return true;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost && at.hostPointer != nullptr;
+}
+
+// Rows [start, start+count) -> caller host buffers.  Pinned caller buffers
+// take the DMA straight (five field copies per table piece); otherwise two
+// pinned staging buffers: block b's field copies run on the copy stream
+// while host threads copy block b-1 out of the other buffer.
 static int get_rows_staged(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
                            int32_t* hops, int32_t* pred, uint8_t* flags) {
     const size_t T = pe->attached.size();
@@ -1242,8 +1285,26 @@ static int get_rows_staged(ShdPe* pe, int32_t start, int32_t count, double* lat,
     std::vector<Piece> pieces;
     int rc = table_pieces(pe, start, count, pieces);
     if (rc) return rc;
+    if (is_pinned(lat) && is_pinned(rel) && is_pinned(hops) && is_pinned(pred) && is_pinned(flags)) {
+        for (const Piece& pc : pieces) {
+            HIPCHK(hipSetDevice(pc.device));
+            const DevTable& tb = *pc.tab;
+            const size_t off = (size_t)(pc.start - tb.rowStart) * T, cells = (size_t)pc.count * T;
+            const size_t o = (size_t)(pc.start - start) * T;
+            if (lat) HIPCHK(hipMemcpyAsync(lat + o, tb.lat + off, cells * 8, hipMemcpyDeviceToHost, pc.stream));
+            if (rel) HIPCHK(hipMemcpyAsync(rel + o, tb.rel + off, cells * 8, hipMemcpyDeviceToHost, pc.stream));
+            if (hops) HIPCHK(hipMemcpyAsync(hops + o, tb.hops + off, cells * 4, hipMemcpyDeviceToHost, pc.stream));
+            if (pred) HIPCHK(hipMemcpyAsync(pred + o, tb.pred + off, cells * 4, hipMemcpyDeviceToHost, pc.stream));
+            if (flags) HIPCHK(hipMemcpyAsync(flags + o, tb.flags + off, cells, hipMemcpyDeviceToHost, pc.stream));
+        }
+        for (const Piece& pc : pieces) {
+            HIPCHK(hipSetDevice(pc.device));
+            HIPCHK(hipStreamSynchronize(pc.stream));
+        }
+        return SHD_PE_OK;
+    }
     if (!pe->stage[0]) {
-        const size_t want = std::max<size_t>(perRow, (size_t)32 << 20);
+        const size_t want = std::max<size_t>(perRow, (size_t)64 << 20);
         for (auto& h : pe->stage)
             HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h), want, hipHostMallocPortable));
         pe->stageBytes = want;
@@ -1266,11 +1327,11 @@ static int get_rows_staged(ShdPe* pe, int32_t start, int32_t count, double* lat,
         auto drain = [&](int buf, Blk b) {
             const unsigned char* q = pe->stage[buf];
             const size_t o = ((size_t)(pc.start - start) + b.r0) * T, cells = (size_t)b.n * T;
-            if (lat) { std::memcpy(lat + o, q, cells * 8); q += cells * 8; }
-            if (rel) { std::memcpy(rel + o, q, cells * 8); q += cells * 8; }
-            if (hops) { std::memcpy(hops + o, q, cells * 4); q += cells * 4; }
-            if (pred) { std::memcpy(pred + o, q, cells * 4); q += cells * 4; }
-            if (flags) std::memcpy(flags + o, q, cells);
+            if (lat) { par_memcpy(lat + o, q, cells * 8); q += cells * 8; }
+            if (rel) { par_memcpy(rel + o, q, cells * 8); q += cells * 8; }
+            if (hops) { par_memcpy(hops + o, q, cells * 4); q += cells * 4; }
+            if (pred) { par_memcpy(pred + o, q, cells * 4); q += cells * 4; }
+            if (flags) par_memcpy(flags + o, q, cells);
         };
         hipEvent_t done[2];
         HIPCHK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
@@ -1313,6 +1374,20 @@ extern "C" int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* 
     int rc = ensure_rows(pe, start, count);
     if (rc) return rc;
     return get_rows_staged(pe, start, count, lat, rel, hops, pred, flags);
+}
+
+extern "C" int shd_pe_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes <= 0) return SHD_PE_EINVAL;
+    *out = nullptr;
+    if (hipHostMalloc(out, (size_t)bytes, hipHostMallocPortable) != hipSuccess) {
+        *out = nullptr;
+        return SHD_PE_ENOMEM;
+    }
+    return SHD_PE_OK;
+}
+
+extern "C" void shd_pe_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, double* dLat,

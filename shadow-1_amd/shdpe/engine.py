@@ -39,6 +39,7 @@ EXPORTS = [
     "shd_graphml_vertex_id", "shd_graphml_free", "shd_rowstore_new", "shd_rowstore_free",
     "shd_rowstore_get", "shd_rowstore_store", "shd_rowstore_store_row", "shd_rowstore_increment",
     "shd_rowstore_size", "shd_rowstore_min_latency", "shd_rowstore_memory_bytes",
+    "shd_pe_host_alloc", "shd_pe_host_free",
 ]
 
 
@@ -145,6 +146,8 @@ def load_library(path: str = LIB_PATH):
         "shd_rowstore_size": (i64, [vp]),
         "shd_rowstore_min_latency": (f64, [vp]),
         "shd_rowstore_memory_bytes": (i64, [vp]),
+        "shd_pe_host_alloc": (C.c_int, [i64, vp]),
+        "shd_pe_host_free": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -161,6 +164,29 @@ def plan_shards(T: int, G: int, unit: int = 1) -> np.ndarray:
     if rc:
         raise EngineError(rc, "shd_pe_plan_shards")
     return b
+
+
+class _PinnedBuf:
+    """Owner of one shd_pe_host_alloc block (freed with the last array view)."""
+
+    def __init__(self, lib, nbytes):
+        self.lib, self.p = lib, C.c_void_p()
+        rc = lib.shd_pe_host_alloc(int(nbytes), C.byref(self.p))
+        if rc:
+            raise EngineError(rc, "shd_pe_host_alloc")
+
+    def __del__(self):
+        if self.p:
+            self.lib.shd_pe_host_free(self.p)
+            self.p = C.c_void_p()
+
+
+def _pinned_array(shape, dtype, lib):
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    buf = _PinnedBuf(lib, max(1, nbytes))
+    raw = (C.c_char * max(1, nbytes)).from_address(buf.p.value)
+    raw._owner = buf                         # keep the block alive with the array
+    return np.frombuffer(raw, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
 
 
 def kernel_source_hash() -> str:
@@ -289,15 +315,34 @@ class Engine:
                                            _p(pred), _p(flags)), "shd_pe_get_row")
         return dict(lat=lat, rel=rel, hops=hops, pred=pred, flags=flags)
 
-    def get_rows(self, start: int, count: int):
-        """Rows [start, start+count) by table position, row-major (count x T)."""
+    def get_rows(self, start: int, count: int, out: dict | None = None):
+        """Rows [start, start+count) by table position, row-major (count x T).
+        `out` (e.g. from pinned_rows) receives them in place."""
         T = self.T
-        lat = np.empty((count, T)); rel = np.empty((count, T))
-        hops = np.empty((count, T), np.int32); flags = np.empty((count, T), np.uint8)
-        pred = np.empty((count, T), np.int32) if self.store_pred else None
+        if out is not None:
+            lat, rel, hops, flags, pred = (out[k][:count] if out.get(k) is not None else None
+                                           for k in ("lat", "rel", "hops", "flags", "pred"))
+        else:
+            lat = np.empty((count, T)); rel = np.empty((count, T))
+            hops = np.empty((count, T), np.int32); flags = np.empty((count, T), np.uint8)
+            pred = np.empty((count, T), np.int32) if self.store_pred else None
         self._chk(self._lib.shd_pe_get_rows(self.h, int(start), int(count), _p(lat), _p(rel),
                                             _p(hops), _p(pred), _p(flags)), "shd_pe_get_rows")
         return dict(lat=lat, rel=rel, hops=hops, pred=pred, flags=flags)
+
+    def pinned_rows(self, count: int) -> dict:
+        """Row buffers for get_rows(out=...) in page-locked host memory
+        (shd_pe_host_alloc): the DMA lands in them without a staging copy.
+        Freed when the returned arrays are garbage collected."""
+        T = self.T
+        out = {}
+        for k, dt in (("lat", np.float64), ("rel", np.float64), ("hops", np.int32),
+                      ("flags", np.uint8), ("pred", np.int32)):
+            if k == "pred" and not self.store_pred:
+                out[k] = None
+                continue
+            out[k] = _pinned_array((count, T), dt, self._lib)
+        return out
 
     def copy_rows_device(self, start, count, d_lat=0, d_rel=0, d_hops=0, d_flags=0):
         self._chk(self._lib.shd_pe_copy_rows_device(
