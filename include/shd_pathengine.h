@@ -135,6 +135,8 @@ typedef struct ShdPeStats {
     int64_t rowsTieEarly;      /* of rowsExact: early-stop emulation (the batch
                                   kernel exported distances, parents and the tie
                                   threshold; k_tie_write wrote the row)          */
+    int32_t batchWaves;        /* k_batch_rows variant in use: waves per SIMD (4
+                                  or 8; shd_pe_tune picks the faster)             */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */
@@ -163,6 +165,12 @@ int shd_pe_attached(const ShdPe* pe, int32_t* outVertices);
 /* Compute all rows this engine owns (eager batch, e.g. on the first cache
  * miss); every local shard on its own device, concurrently. */
 int shd_pe_compute_all(ShdPe* pe);
+
+/* Optional, once, before timed or production use: computes the engine's
+ * own rows with each k_batch_rows variant (8 / 4 waves per SIMD) and keeps
+ * the faster for later calls (their ranking differs between boxes of the
+ * same SKU).  The table is left fully computed; no-op on other paths. */
+int shd_pe_tune(ShdPe* pe);
 
 /* Compute rows for the given sources (vertex ids, must be attached). */
 int shd_pe_compute_rows(ShdPe* pe, const int32_t* srcVertices, int32_t count);

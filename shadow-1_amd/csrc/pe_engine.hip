@@ -63,6 +63,8 @@ struct Shard {
     SparseLaunch cfg{};
     int exactGrid = 0, exactHc = 1;
     BatchLaunch bcfg{};
+    BatchLaunch bcfgAlt{};          // the other kernel variant (grid 0: none), shd_pe_tune
+    bool tuned = false;
     BatchScratch bsc{};
     bool batchReady = false;
     int32_t* dBatchRows = nullptr;
@@ -270,8 +272,6 @@ static int configure(ShdPe* pe, Shard* sh) {
         b.lb = ((int64_t)sh->rowCount + 15) / 16 < (int64_t)sh->numCUs ? 8 : 16;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
-    // kernel variant: 8 waves per SIMD (two workgroups per CU) when two fit
-    // the CU's LDS, else 4 (SHDPE_BATCH_WPE forces one) ...
     // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
     // control block, else in each slot's global scratch (gbits, LB 16)
     b.gbits = pe->batched && batch_lds_bytes((int)n, 8, false) > LDS ? 1 : 0;
@@ -287,25 +287,38 @@ static int configure(ShdPe* pe, Shard* sh) {
             per = 0;
         return per;
     };
-    // (and only when the shard has a batch for every one of those workgroups:
-    // C4 per-rank shard times N = 4 / 8, profiles/r02l_shard_times.txt)
-    const int64_t nBatchesAll = ((int64_t)sh->rowCount + b.lb - 1) / b.lb;
-    b.wpe = tu.batchWpe == 4 || tu.batchWpe == 8
-                ? tu.batchWpe
-                : (nBatchesAll >= 2LL * sh->numCUs && occupancy(8) >= 2 ? 8 : 4);
-    b.ldsBytes = batch_lds_bytes((int)n, b.wpe, b.gbits != 0);
-    if (pe->batched && b.ldsBytes > LDS) return SHD_PE_ETOOBIG;
+    // Two kernel variants: 8 waves per SIMD (two 1024-thread workgroups per
+    // CU, one vertex per group) and 4 (one workgroup per CU, two vertices
+    // per group).  Which is faster differs from box to box of the same SKU
+    // (C4 same-box pairs: 172 vs 185 ms on some, 182 vs 142 ms on others;
+    // profiles/r03_ab_notes.txt), so the engine starts with 8 and
+    // shd_pe_tune times both; SHDPE_BATCH_WPE forces one.
+    auto make = [&](int wpe) {
+        BatchLaunch c = b;
+        c.wpe = wpe;
+        c.ldsBytes = batch_lds_bytes((int)n, wpe, b.gbits != 0);
+        const int per = c.ldsBytes <= LDS ? occupancy(wpe) : 0;
+        c.grid = sh->numCUs * std::max(per, 1);
+        if (tu.batchGrid > 0 && tu.batchGrid < c.grid) c.grid = tu.batchGrid;
+        c.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
+        if (!(c.delta > 0)) c.delta = 1.0;
+        return std::make_pair(c, per);
+    };
+    const int forced = tu.batchWpe == 4 || tu.batchWpe == 8 ? tu.batchWpe : 0;
+    auto v8 = make(8), v4 = make(4);
+    const bool ok8 = v8.second >= 1, ok4 = v4.second >= 1;
+    if (pe->batched && !ok8 && !ok4) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
-    int bPerCU = b.ldsBytes <= LDS ? occupancy(b.wpe) : 1;
-    if (bPerCU < 1) bPerCU = 1;
-    b.grid = sh->numCUs * bPerCU;
-    if (tu.batchGrid > 0 && tu.batchGrid < b.grid) b.grid = tu.batchGrid;
-    b.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
-    if (!(b.delta > 0)) b.delta = 1.0;
+    const int first = forced ? forced : (ok8 ? 8 : 4);
+    b = first == 8 ? v8.first : v4.first;
+    sh->bcfgAlt = BatchLaunch{};
+    if (!forced && ok8 && ok4) sh->bcfgAlt = first == 8 ? v4.first : v8.first;
+    (void)need0;
     sh->bcfg = b;
     sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
     sh->stats.batched = pe->batched ? 1 : 0;
     sh->stats.batchLanes = pe->batched ? b.lb : 0;
+    sh->stats.batchWaves = pe->batched ? b.wpe : 0;
     return SHD_PE_OK;
 }
 
@@ -780,8 +793,10 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
     const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
-    const size_t slots = std::min<size_t>({(size_t)sh->bcfg.grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
-    sh->bcfg.grid = (int32_t)slots;
+    const size_t grid = (size_t)std::max(sh->bcfg.grid, sh->bcfgAlt.grid);
+    const size_t slots = std::min<size_t>({grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
+    sh->bcfg.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfg.grid);
+    if (sh->bcfgAlt.grid > 0) sh->bcfgAlt.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt.grid);
     int rc;
     void *D, *R, *H, *P, *q, *rows, *amb;
     if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
@@ -1173,6 +1188,43 @@ extern "C" int shd_pe_compute_positions(ShdPe* pe, int32_t start, int32_t count)
 extern "C" int shd_pe_compute_all(ShdPe* pe) {
     if (!pe) return SHD_PE_EINVAL;
     return shd_pe_compute_positions(pe, pe->ownStart, pe->ownEnd - pe->ownStart);
+}
+
+extern "C" int shd_pe_tune(ShdPe* pe) {
+    if (!pe) return SHD_PE_EINVAL;
+    if (!pe->batched) return SHD_PE_OK;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    for (auto& sp : pe->shards) {
+        Shard* sh = sp.get();
+        if (sh->tuned || sh->bcfgAlt.grid <= 0 || sh->rowCount <= 0) continue;
+        std::vector<int32_t> pos(sh->rowCount);
+        for (int32_t i = 0; i < sh->rowCount; ++i) pos[i] = sh->rowStart + i;
+        const ShdPeStats keep = sh->stats;
+        double ms[2] = {0.0, 0.0};
+        int w[2] = {0, 0};
+        for (int k = 0; k < 2; ++k) {
+            w[k] = sh->bcfg.wpe;
+            // a first launch of each variant maps its code and scratch; the
+            // second is timed
+            for (int rep = 0; rep < 2; ++rep) {
+                const double m0 = sh->stats.msSparseKernel;
+                int rc = compute_shard(pe, sh, pos.data(), sh->rowCount);
+                if (rc) { sh->stats = keep; return rc; }
+                ms[k] = sh->stats.msSparseKernel - m0;
+            }
+            std::swap(sh->bcfg, sh->bcfgAlt);
+        }
+        // ms[0]: the starting variant, ms[1]: the alternative (now in bcfgAlt
+        // again after the second swap)
+        if (ms[1] < ms[0]) std::swap(sh->bcfg, sh->bcfgAlt);
+        sh->tuned = true;
+        sh->stats = keep;
+        sh->stats.batchWaves = sh->bcfg.wpe;
+        if (pe->tu.debug)
+            std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms, %d waves %.2f ms -> %d\n",
+                         sh->gindex, w[0], ms[0], w[1], ms[1], sh->bcfg.wpe);
+    }
+    return SHD_PE_OK;
 }
 
 extern "C" int shd_pe_compute_rows(ShdPe* pe, const int32_t* src, int32_t count) {
@@ -1753,6 +1805,7 @@ extern "C" int shd_pe_reset_stats(ShdPe* pe) {
         st.deltaUsed = keep.deltaUsed;
         st.batched = keep.batched;
         st.batchLanes = keep.batchLanes;
+        st.batchWaves = keep.batchWaves;
     }
     pe->msGather = 0.0;
     return SHD_PE_OK;

@@ -39,7 +39,7 @@ EXPORTS = [
     "shd_graphml_vertex_id", "shd_graphml_free", "shd_rowstore_new", "shd_rowstore_free",
     "shd_rowstore_get", "shd_rowstore_store", "shd_rowstore_store_row", "shd_rowstore_increment",
     "shd_rowstore_size", "shd_rowstore_min_latency", "shd_rowstore_memory_bytes",
-    "shd_pe_host_alloc", "shd_pe_host_free",
+    "shd_pe_host_alloc", "shd_pe_host_free", "shd_pe_tune",
 ]
 
 
@@ -67,7 +67,7 @@ class Stats(C.Structure):
                 ("msDenseKernel", C.c_double), ("launchesDense", C.c_int64),
                 ("denseSweeps", C.c_int64), ("denseFlops", C.c_double),
                 ("batched", C.c_int32), ("batchLanes", C.c_int32), ("nShards", C.c_int32),
-                ("msGather", C.c_double), ("rowsTieEarly", C.c_int64)]
+                ("msGather", C.c_double), ("rowsTieEarly", C.c_int64), ("batchWaves", C.c_int32)]
 
 
 class EngineError(RuntimeError):
@@ -148,6 +148,7 @@ def load_library(path: str = LIB_PATH):
         "shd_rowstore_memory_bytes": (i64, [vp]),
         "shd_pe_host_alloc": (C.c_int, [i64, vp]),
         "shd_pe_host_free": (None, [vp]),
+        "shd_pe_tune": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -348,6 +349,11 @@ class Engine:
         self._chk(self._lib.shd_pe_copy_rows_device(
             self.h, int(start), int(count), d_lat or None, d_rel or None, d_hops or None,
             d_flags or None), "shd_pe_copy_rows_device")
+
+    def tune(self):
+        """shd_pe_tune: time both k_batch_rows variants on this engine's rows,
+        keep the faster (leaves the table computed)."""
+        self._chk(self._lib.shd_pe_tune(self.h), "shd_pe_tune")
 
     def stats(self) -> dict:
         s = Stats()

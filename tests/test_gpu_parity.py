@@ -515,6 +515,27 @@ def test_large_graph_batched_kernel(E, oracle_mod, n):
     assert st["mode"] == 1 and st["batched"] == 1
 
 
+def test_tune_picks_a_variant_and_keeps_parity(E, oracle_mod):
+    """shd_pe_tune times both k_batch_rows variants (8 / 4 waves per SIMD)
+    on the engine's rows and keeps the faster; the table it leaves and every
+    later compute stay bit-exact."""
+    top = G.power_law(30_000, 3, seed=5)
+    att = np.arange(0, top.n, 7, dtype=np.int32)
+    eng = E.Engine(top, att, force_mode=5)
+    eng.tune()
+    st = eng.stats()
+    assert st["batched"] == 1 and st["batchWaves"] in (4, 8) and st["rowsComputed"] == 0
+    og = oracle_mod.OracleGraph(top)
+    pos = np.arange(0, eng.T, 97)
+    exp = og.rows(eng.attached[pos], eng.attached, threads=8)
+    for rnd in range(2):               # the tuned table, then a fresh compute
+        for i, p in enumerate(pos):
+            got = {k: (v[0] if v is not None else None) for k, v in eng.get_rows(int(p), 1).items()}
+            _assert_rows_equal(got, {k: v[i] for k, v in exp.items()}, f"round {rnd} row {p}")
+        eng.compute_all()
+    eng.close()
+
+
 def _twin_tie_graph(z_attached, seed=11):
     """A tie-free random graph plus twins a, b (both hanging off hub h with
     the same latency) and z adjacent to exactly a and b with equal latency:

@@ -53,6 +53,20 @@ for st in ${STAGES:-tests bench}; do
       (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace_$wl -o trace -- python3 $R/bench.py --workload $wl --steps 5 --warmup 1 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $R/$OUT/trace_$wl.json 2> $R/$OUT/trace_$wl.err) || { tail -20 $OUT/trace_$wl.err; exit 1; }
       line $OUT/trace_$wl.json "$wl traced"
     done ;;
+  default)
+    # the driver's command: python bench.py (defaults: C4, CPU legs, tie stress, D2H)
+    timeout -k 10 600 python3 -u bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { tail -20 $OUT/bench_default.err; exit 1; }
+    line $OUT/bench_default.json "default" ;;
+  envsweep)
+    # one line per environment setting in $ENVS (';'-separated lists of VAR=VAL)
+    IFS=';' read -ra ES <<< "${ENVS:-}"
+    for e in "${ES[@]}"; do
+      for wl in ${WLS//,/ }; do
+        env $e SHDPE_DEBUG=${ABDEBUG:-0} timeout -k 10 300 python3 -u bench.py --workload $wl --steps 3 --warmup 1 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $OUT/env.json 2> $OUT/env.err || { tail -20 $OUT/env.err; exit 1; }
+        line $OUT/env.json "$wl [$e]"
+        if [ -n "$ABDEBUG" ]; then grep shdpe $OUT/env.err | head -8; fi
+      done
+    done ;;
   relabel)
     timeout -k 10 400 python3 -u tools/relabel_probe.py ${RELABEL_WL:-c4} > $OUT/relabel.txt 2>&1 || { tail -20 $OUT/relabel.txt; exit 1; }
     cat $OUT/relabel.txt ;;

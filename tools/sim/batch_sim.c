@@ -15,6 +15,9 @@
 
 typedef struct {
     double procs, arcs, phases, lanesAct, cands;
+    double touched;     // distinct (vertex, phase) pairs relaxed into (any lane, improving or not)
+    double improving;   // arc visits with at least one improving lane
+    double laneImp;     // improving lane relaxations
 } SimOut;
 
 int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double* lat,
@@ -26,6 +29,9 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     int32_t* q = malloc(sizeof(int32_t) * n);
     uint64_t* dirty = calloc(n, 8);
     uint8_t* farp = calloc(n, 1);
+    int32_t* stamp = malloc(sizeof(int32_t) * n);
+    for (int v = 0; v < n; ++v) stamp[v] = -1;
+    int32_t gphase = 0;
     if (!D || !pend || !nextp || !q) return -1;
     memset(out, 0, sizeof(*out));
     for (int b = 0; b < nBatch; ++b) {
@@ -71,6 +77,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
             }
             memset(pend, 0, n);
             memset(nextp, 0, n);
+            ++gphase;
             int active = 0;
             double minNext = INFINITY;
             out->cands += qn;
@@ -106,6 +113,8 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 for (int a = rowPtr[u]; a < rowPtr[u + 1]; ++a) {
                     const int x = col[a];
                     const double w = lat[a];
+                    if (stamp[x] != gphase) { stamp[x] = gphase; out->touched += 1; }
+                    int anyImp = 0;
                     for (int l = 0; l < LB; ++l) {
                         if (!((act >> l) & 1)) continue;
                         const double nb = du[l] + w;
@@ -119,8 +128,11 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                             }
                             dirty[x] |= 1ull << l;
                             active = 1;
+                            anyImp = 1;
+                            out->laneImp += 1;
                         }
                     }
+                    out->improving += anyImp;
                 }
             }
             memcpy(pend, nextp, n);
@@ -139,5 +151,6 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     free(q);
     free(dirty);
     free(farp);
+    free(stamp);
     return 0;
 }

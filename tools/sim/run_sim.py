@@ -18,7 +18,8 @@ from shdpe import generators as G  # noqa: E402
 
 class Out(ctypes.Structure):
     _fields_ = [("procs", ctypes.c_double), ("arcs", ctypes.c_double),
-                ("phases", ctypes.c_double), ("lanesAct", ctypes.c_double), ("cands", ctypes.c_double)]
+                ("phases", ctypes.c_double), ("lanesAct", ctypes.c_double), ("cands", ctypes.c_double),
+                ("touched", ctypes.c_double), ("improving", ctypes.c_double), ("laneImp", ctypes.c_double)]
 
 
 def lib():
@@ -72,6 +73,7 @@ def run(L, rp, col, w, n, batches, offs, LB, delta, heavy=64, dirty=0, far=0):
                      ctypes.c_int32(heavy), ctypes.c_int32(dirty), ctypes.c_int32(far), ctypes.byref(out))
     assert rc == 0
     run.cands = out.cands / nb / n
+    run.extra = (out.touched / nb / col.shape[0], out.improving / nb / col.shape[0], out.laneImp / nb / n / LB)
     return out.procs / nb / n, out.arcs / nb / col.shape[0], out.phases / nb
 
 
