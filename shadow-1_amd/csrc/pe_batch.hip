@@ -52,6 +52,18 @@ template <int WPE> struct BCfg {
     static constexpr int SMAX = WPE >= 8 ? 8 : 16;   // label-walk stack: (entry, arc) pairs per thread
 };
 constexpr int WALK_BUDGET = 2048;   // walk steps per target before the deep-tree sweeps
+// Lane policy of the relaxation: a vertex with ANY dirty lane below the
+// bucket bound relaxes ALL its dirty lanes (eager) instead of only those
+// below the bound.  The lanes of a batch reach a vertex in different
+// buckets; taking the late ones along with the first costs some label-
+// correcting re-relaxations but saves whole vertex visits (each visit reads
+// one [v][LB] line per arc): C4 schedule simulation (tools/sim) 2.21 -> 1.56
+// arc visits per batch, x m_arcs, at a quarter of the bucket width.
+#ifdef SHDPE_X_LANE_POLICY
+constexpr bool EAGER = false;
+#else
+constexpr bool EAGER = true;
+#endif
 
 struct alignas(16) BCtrl {
     int qtail;
@@ -357,8 +369,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
                     const double k0 = b2d(dec(e0)) + sh;
                     const bool dirty = !(e0 & 1ull);
-                    const bool act = dirty && k0 < bound;
-                    const bool defer = dirty && !(k0 < bound);
+                    const bool below = dirty && k0 < bound;
+                    const bool act = EAGER ? dirty && __ballot(below) >> gbase & LBMASK : below;
+                    const bool defer = dirty && !act;
                     const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
                     const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
                     if (gw == 0 && l == 0 && dmask) anyF.set(u);
@@ -450,8 +463,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 for (int v = 0; v < BV; ++v) {
                     const double k0 = b2d(dec(db[v])) + sh;
                     const bool dirty = !(db[v] & 1ull);
-                    const bool act = dirty && k0 < bound;
-                    const bool defer = dirty && !(k0 < bound);
+                    const bool below = dirty && k0 < bound;
+                    const bool act = EAGER ? dirty && __ballot(below) >> gbase & LBMASK : below;
+                    const bool defer = dirty && !act;
                     const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
                     const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
                     if (l == 0 && dmask) anyF.set(u[v]);

@@ -20,9 +20,12 @@ typedef struct {
     double laneImp;     // improving lane relaxations
 } SimOut;
 
+// vkey (optional, [nBatch][n]): a per-VERTEX bucket key replacing every
+// lane's dist - off (scheduling experiments: all lanes of a vertex processed
+// together at the vertex's key).
 int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double* lat,
               const int32_t* srcs, const double* offs, int32_t nBatch, int32_t LB, double delta,
-              int32_t heavyDeg, int32_t dirtyMode, int32_t farMode, SimOut* out) {
+              int32_t heavyDeg, int32_t dirtyMode, int32_t farMode, SimOut* out, const double* vkey) {
     double* D = malloc(sizeof(double) * (size_t)n * LB);
     uint8_t* pend = calloc(n, 1);
     uint8_t* nextp = calloc(n, 1);
@@ -37,6 +40,8 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     for (int b = 0; b < nBatch; ++b) {
         const int32_t* s = srcs + (size_t)b * LB;
         const double* off = offs + (size_t)b * LB;
+        const double* vk = vkey ? vkey + (size_t)b * n : NULL;
+#define KEY(v, l, d) (vk ? vk[v] : (d) - off[l])
         for (size_t i = 0; i < (size_t)n * LB; ++i) D[i] = INFINITY;
         memset(pend, 0, n);
         memset(dirty, 0, 8 * (size_t)n);
@@ -88,7 +93,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 for (int l = 0; l < LB; ++l) {
                     du[l] = D[(size_t)u * LB + l];
                     if (du[l] == INFINITY) continue;
-                    const double key = du[l] - off[l];
+                    const double key = KEY(u, l, du[l]);
                     if (key < bound) act |= 1ull << l;
                     else if (farMode) {
                         farp[u] = 1;
@@ -97,6 +102,11 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                         nextp[u] = 1;
                         if (key < minNext) minNext = key;
                     }
+                }
+                if ((farMode & 2) && act) {
+                    // eager: every reached lane of u goes with the active ones
+                    for (int l = 0; l < LB; ++l)
+                        if (du[l] != INFINITY) act |= 1ull << l;
                 }
                 if (dirtyMode) {
                     uint64_t dm = 0;
@@ -120,9 +130,9 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                         const double nb = du[l] + w;
                         if (nb < D[(size_t)x * LB + l]) {
                             D[(size_t)x * LB + l] = nb;
-                            if (farMode && nb - off[l] >= bound) {
+                            if (farMode && KEY(x, l, nb) >= bound) {
                                 farp[x] = 1;
-                                if (nb - off[l] < farMin) farMin = nb - off[l];
+                                if (KEY(x, l, nb) < farMin) farMin = KEY(x, l, nb);
                             } else {
                                 nextp[x] = 1;
                             }

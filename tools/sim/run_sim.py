@@ -63,14 +63,15 @@ def hub_assign(rp, col, w, n, K):
     return src, d
 
 
-def run(L, rp, col, w, n, batches, offs, LB, delta, heavy=64, dirty=0, far=0):
+def run(L, rp, col, w, n, batches, offs, LB, delta, heavy=64, dirty=0, far=0, vkey=None):
     out = Out()
     nb = batches.shape[0] // LB
     rc = L.batch_sim(ctypes.c_int32(n), rp.ctypes.data_as(ctypes.c_void_p),
                      col.ctypes.data_as(ctypes.c_void_p), w.ctypes.data_as(ctypes.c_void_p),
                      batches.ctypes.data_as(ctypes.c_void_p), offs.ctypes.data_as(ctypes.c_void_p),
                      ctypes.c_int32(nb), ctypes.c_int32(LB), ctypes.c_double(delta),
-                     ctypes.c_int32(heavy), ctypes.c_int32(dirty), ctypes.c_int32(far), ctypes.byref(out))
+                     ctypes.c_int32(heavy), ctypes.c_int32(dirty), ctypes.c_int32(far), ctypes.byref(out),
+                     None if vkey is None else np.ascontiguousarray(vkey, np.float64).ctypes.data_as(ctypes.c_void_p))
     assert rc == 0
     run.cands = out.cands / nb / n
     run.extra = (out.touched / nb / col.shape[0], out.improving / nb / col.shape[0], out.laneImp / nb / n / LB)
