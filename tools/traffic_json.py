@@ -26,15 +26,27 @@ KERNELS = ("k_batch_rows", "k_sparse_rows", "k_minplus", "k_direct_rows")
 def main():
     outdir, wl, tag = sys.argv[1], sys.argv[2], sys.argv[3]
     dst = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles", f"traffic_{wl}.json")
-    tot = defaultdict(lambda: defaultdict(float))
-    disp = defaultdict(lambda: defaultdict(set))
+    # per pass, only the LAST dispatch of each path kernel: bench.py runs
+    # shd_pe_tune (both kernel variants) before the measured step
+    last = {}
+    rows = defaultdict(list)
     for f in glob.glob(os.path.join(outdir, f"pmc_{wl}_*", "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = next((k for k in KERNELS if k in r.get("Kernel_Name", "")), None)
             if k is None:
                 continue
+            d = int(r.get("Dispatch_Id") or 0)
+            key = (f, k)
+            last[key] = max(last.get(key, -1), d)
+            rows[key].append((d, r))
+    tot = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(lambda: defaultdict(set))
+    for (f, k), rs in rows.items():
+        for d, r in rs:
+            if d != last[(f, k)]:
+                continue
             tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[k][r["Counter_Name"]].add((f, r.get("Dispatch_Id")))
+            disp[k][r["Counter_Name"]].add((f, d))
     if not tot:
         sys.exit(f"no counters for the path kernels under {outdir}/pmc_{wl}_*")
     k = max(tot, key=lambda x: tot[x].get("FETCH_SIZE", 0.0))
@@ -52,6 +64,7 @@ def main():
         "write_bytes": write,
         "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
         "launches_per_pass": nl,
+        "dispatch": "the last launch of the pass (the measured step; the tuning launches before it are ignored)",
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, KB*1024, "
                   "bench.py --steps 1 --warmup 0 (one launch).  Reads = 2 x FETCH_SIZE (gfx950 "
                   "calibration for random 128-B lines, profiles/r02e_fetch_calibration.json); "
