@@ -72,7 +72,7 @@ struct alignas(16) BCtrl {
     unsigned int ambMask;
     int changed;
     int htail;        // heavy-vertex list (grows down from the top of the queue)
-    int pad;
+    int qhead;        // next light-queue entry to take (dynamic distribution)
     unsigned long long busyMax;
     unsigned long long busySum;
     double maxOff;    // largest lane offset of the batch (bits via atomicMax)
@@ -247,6 +247,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             for (int w = tid; w < nwp; w += NT) { any0.st(w, 0u); any1.st(w, 0u); }
             if (tid == 0) {
                 ctl->qtail = 0;
+                ctl->qhead = 0;
                 ctl->farAny = 0;
                 ctl->farMin = INF_BITS;
                 ctl->ambMask = 0u;
@@ -429,25 +430,29 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     }
                 }
             }
-            // the queue entries of the group's NEXT vertices are loaded one
-            // iteration ahead (qn >= 1 here), so a vertex starts with its
-            // dist / row-range loads instead of a dependent queue round trip
+            // Groups take BV queue entries at a time from an LDS counter, so
+            // the phase ends when the last entry is done rather than when the
+            // unluckiest static share is.  The entries of a group's NEXT take
+            // are loaded one iteration ahead, so a vertex starts with its dist
+            // / row-range loads instead of a dependent queue round trip.
+            const int qc = qn > 0 ? qn - 1 : 0;
+            auto take = [&]() {
+                int i = 0;
+                if (l == 0) i = atomicAdd(&ctl->qhead, BV);
+                return __shfl(i, gbase, 64);
+            };
+            int i0 = take();
             int nq[BV];
 #pragma unroll
-            for (int v = 0; v < BV; ++v) {
-                const int idx = gid * BV + v;
-                nq[v] = qn > 0 ? ld_wg(&Q[idx < qn ? idx : qn - 1]) : -1;
-            }
-            for (int i0 = gid * BV; i0 < qn; i0 += NG * BV) {
+            for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i0 + v, qc)]);
+            while (i0 < qn) {
                 int u[BV], a0[BV], a1[BV];
                 unsigned long long db[BV], dub[BV];
 #pragma unroll
                 for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? nq[v] : -1;
+                const int i1 = take();
 #pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    const int idx = i0 + NG * BV + v;
-                    nq[v] = ld_wg(&Q[idx < qn ? idx : qn - 1]);
-                }
+                for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i1 + v, qc)]);
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
                     // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
@@ -533,6 +538,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             }
                         }
                 }
+                i0 = i1;
             }
             if (dbg && l == 0) {
                 const unsigned long long bz = (unsigned long long)((long long)clock64() - tg0);
@@ -544,6 +550,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
             if (tid == 0) {
                 ctl->qtail = 0;
+                ctl->qhead = 0;
                 ctl->htail = 0;
                 if (dbg) {
                     dbg[16 * b + 12] += (int)(ctl->busyMax >> 10);
