@@ -200,6 +200,21 @@ int shd_pe_get_row(ShdPe* pe, int32_t srcVertex, double* lat, double* rel,
 int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* lat, double* rel,
                     int32_t* hops, int32_t* pred, uint8_t* flags);
 
+/* The igraph shortest path from srcVertex to dstVertex (both attached) as
+ * the vertex sequence [src, ..., dst] in verts (cap entries), *len = its
+ * length: what topology.c builds hop by hop into its path string
+ * (_topology_computePathProperties :1449, :1502-1503, logged by
+ * _topology_computeSourcePaths :1831-1841).  The table keeps only each
+ * target's predecessor, so the first call for a source re-runs igraph's
+ * Dijkstra for it on the device (the exact 2-wheap emulation, one wave:
+ * milliseconds to ~1 s at 10^5 vertices); later calls for the same source
+ * are a device walk until the next compute.  src == dst -> [src]; complete
+ * graphs -> [src, dst] (_topology_lookupDirectPath).  SHD_PE_ENOTOWNED for a
+ * source outside this engine's shard, SHD_PE_EUNREACHABLE, SHD_PE_EINVAL when
+ * the path needs more than cap entries. */
+int shd_pe_get_path(ShdPe* pe, int32_t srcVertex, int32_t dstVertex, int32_t* verts,
+                    int32_t cap, int32_t* len);
+
 /* Page-locked host memory for shd_pe_get_rows destinations (DMA target, no
  * staging copy).  No reference counterpart: Shadow's row buffers are plain
  * g_new allocations (topology.c:1805-1864). */
@@ -323,6 +338,15 @@ int shd_rowstore_increment(ShdRowStore* st, int32_t s, int32_t d);
 int64_t shd_rowstore_size(const ShdRowStore* st);
 double shd_rowstore_min_latency(const ShdRowStore* st);
 int64_t shd_rowstore_memory_bytes(const ShdRowStore* st);
+
+/* Every cached entry, as stored (src, dst in the stored direction), for the
+ * teardown dump (_topology_logAllCachedPaths, topology.c:1929-1967, which
+ * walks the two-level GHashTable in hash order; here by smaller attached
+ * ordinal).  Not safe against concurrent inserts.  Returns the number of
+ * entries visited. */
+typedef void (*ShdRowStoreVisit)(int32_t src, int32_t dst, double latency, double reliability,
+                                 int32_t isDirect, uint64_t packetCount, void* user);
+int64_t shd_rowstore_foreach(const ShdRowStore* st, ShdRowStoreVisit visit, void* user);
 
 /* ------------------------------------------------------------------------
  * Host mirror of the topology.c path API (the drop-in seen by worker.c,

@@ -59,6 +59,8 @@ struct Shard {
     int32_t* dRows = nullptr;
     uint8_t* dRowAmbig = nullptr;
     int32_t* dDbg = nullptr;
+    int32_t pathSrc = -1;           // source whose full parent array sits in exact slot 0
+    int32_t* dPath = nullptr;       // path walk output (+ length), shd_pe_get_path
     int32_t rowsCap = 0;
     SparseLaunch cfg{};
     int exactGrid = 0, exactHc = 1;
@@ -97,6 +99,7 @@ struct ShdPe {
     bool batched = false;
     std::vector<int32_t> rank;       // table position -> batch order rank
     std::vector<double> rowOff;      // table position -> distance to its batch hub (order 1)
+    std::vector<int32_t> devOf;      // caller vertex id -> device id (empty: identity)
     int G = 1;                       // global row shards
     std::vector<int32_t> bounds;     // G + 1 position bounds
     int firstShard = 0;              // global index of shards[0]
@@ -599,6 +602,10 @@ static int init_shard(ShdPe* pe, Shard* sh) {
             return g.rowPtr[a + 1] - g.rowPtr[a] > g.rowPtr[b + 1] - g.rowPtr[b];
         });
         if ((rc = upload_graph(pe, sh, &sh->dg, &oldOf))) return rc;
+        if (pe->devOf.empty()) {
+            pe->devOf.assign(n, 0);
+            for (int32_t k = 0; k < n; ++k) pe->devOf[oldOf[k]] = k;
+        }
     }
     sh->stats.mode = pe->mode;
     sh->stats.isComplete = g.isComplete ? 1 : 0;
@@ -940,6 +947,7 @@ static void print_exact_debug(Shard* sh, const std::vector<int32_t>& rows, int32
 // Compute the given table positions (all owned by `sh`), chunked.
 static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count) {
     if (count <= 0) return SHD_PE_OK;
+    sh->pathSrc = -1;               // the exact kernels reuse slot 0
     if (hipSetDevice(sh->device) != hipSuccess) return SHD_PE_EHIP;
     int rc = ensure_table(pe, sh);
     if (rc) return rc;
@@ -1426,6 +1434,67 @@ extern "C" int shd_pe_get_rows(ShdPe* pe, int32_t start, int32_t count, double* 
     int rc = ensure_rows(pe, start, count);
     if (rc) return rc;
     return get_rows_staged(pe, start, count, lat, rel, hops, pred, flags);
+}
+
+extern "C" int shd_pe_get_path(ShdPe* pe, int32_t srcVertex, int32_t dstVertex, int32_t* verts,
+                               int32_t cap, int32_t* len) {
+    if (!pe || !verts || !len || cap < 1) return SHD_PE_EINVAL;
+    *len = 0;
+    const HostGraph& g = pe->hg;
+    if (srcVertex < 0 || srcVertex >= g.n || dstVertex < 0 || dstVertex >= g.n) return SHD_PE_EINVAL;
+    const int32_t ps = pe->posOf[srcVertex];
+    if (ps < 0 || pe->posOf[dstVertex] < 0) return SHD_PE_ENOTATTACHED;
+    if (srcVertex == dstVertex) {            // the 1-vertex igraph path [s] (:1469-1488)
+        verts[0] = srcVertex;
+        *len = 1;
+        return SHD_PE_OK;
+    }
+    if (pe->mode == 2) {                     // complete graph: the direct edge (:1877-1927)
+        if (cap < 2) return SHD_PE_EINVAL;
+        if (g.findArc(srcVertex, dstVertex) < 0) return SHD_PE_ENOEDGE;
+        verts[0] = srcVertex;
+        verts[1] = dstVertex;
+        *len = 2;
+        return SHD_PE_OK;
+    }
+    std::lock_guard<std::mutex> lk(pe->mu);
+    Shard* sh = owner_of(pe, ps);
+    if (!sh) return SHD_PE_ENOTOWNED;
+    HIPCHK(hipSetDevice(sh->device));
+    int rc = ensure_table(pe, sh);
+    if (rc) return rc;
+    if (!sh->dPath) {
+        void* p;
+        if ((rc = dev_alloc(sh, &p, ((size_t)g.n + 64) * 4))) return rc;
+        sh->dPath = (int32_t*)p;
+    }
+    if (sh->pathSrc != srcVertex) {
+        // igraph's whole Dijkstra for this source (full 2-wheap emulation,
+        // one wave): every vertex popped before the last target keeps its
+        // chosen IN-arc in slot 0; the row it rewrites is the table's own
+        HIPCHK(hipMemcpyAsync(sh->dRows, &ps, 4, hipMemcpyHostToDevice, sh->stream));
+        launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, 1, 1, sh->exactHc, pe->tu.exactHc > 0,
+                          nullptr, sh->tie, nullptr, sh->stream);
+        HIPCHK(hipGetLastError());
+        sh->pathSrc = srcVertex;
+    }
+    int32_t* dLen = sh->dPath + g.n + 32;
+    // device ids of s and t (the batched path relabels vertices)
+    int32_t sD = srcVertex, tD = dstVertex;
+    if (!pe->devOf.empty()) { sD = pe->devOf[srcVertex]; tD = pe->devOf[dstVertex]; }
+    launch_path_walk(sh->dg, sh->sc.pred, sD, tD, sh->dPath, std::min<int32_t>(cap, g.n + 1), dLen,
+                     sh->stream);
+    HIPCHK(hipGetLastError());
+    int32_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, dLen, 4, hipMemcpyDeviceToHost, sh->stream));
+    HIPCHK(hipStreamSynchronize(sh->stream));
+    if (n == -2) return SHD_PE_EINVAL;            // cap too small for the path
+    if (n < 0) return SHD_PE_EUNREACHABLE;
+    std::vector<int32_t> rev(n);
+    HIPCHK(hipMemcpy(rev.data(), sh->dPath, (size_t)n * 4, hipMemcpyDeviceToHost));
+    for (int32_t k = 0; k < n; ++k) verts[k] = rev[n - 1 - k];
+    *len = n;
+    return SHD_PE_OK;
 }
 
 extern "C" int shd_pe_host_alloc(int64_t bytes, void** out) {

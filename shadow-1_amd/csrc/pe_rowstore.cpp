@@ -222,3 +222,22 @@ extern "C" int64_t shd_rowstore_memory_bytes(const ShdRowStore* st) {
                     (int64_t)st->n * 4
               : 0;
 }
+
+extern "C" int64_t shd_rowstore_foreach(const ShdRowStore* st, ShdRowStoreVisit visit, void* user) {
+    if (!st || !visit) return 0;
+    int64_t cnt = 0;
+    for (int32_t a = 0; a < st->T; ++a) {
+        const TriRow* r = st->rows[a].load(std::memory_order_acquire);
+        if (!r) continue;
+        for (int32_t k = 0; a + k < st->T; ++k) {
+            const uint8_t x = r->state[k].load(std::memory_order_acquire);
+            if (!(x & S_STORED)) continue;
+            const int32_t va = st->attached[a], vb = st->attached[a + k];
+            const bool rev = (x & S_REVERSED) != 0;     // stored under (larger, smaller)
+            visit(rev ? vb : va, rev ? va : vb, r->lat[k], r->rel[k], (x & S_DIRECT) ? 1 : 0,
+                  r->packets[k].load(std::memory_order_relaxed), user);
+            ++cnt;
+        }
+    }
+    return cnt;
+}

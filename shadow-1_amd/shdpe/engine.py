@@ -39,7 +39,8 @@ EXPORTS = [
     "shd_graphml_vertex_id", "shd_graphml_free", "shd_rowstore_new", "shd_rowstore_free",
     "shd_rowstore_get", "shd_rowstore_store", "shd_rowstore_store_row", "shd_rowstore_increment",
     "shd_rowstore_size", "shd_rowstore_min_latency", "shd_rowstore_memory_bytes",
-    "shd_pe_host_alloc", "shd_pe_host_free", "shd_pe_tune",
+    "shd_pe_host_alloc", "shd_pe_host_free", "shd_pe_tune", "shd_pe_get_path",
+    "shd_rowstore_foreach",
 ]
 
 
@@ -149,6 +150,8 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_host_alloc": (C.c_int, [i64, vp]),
         "shd_pe_host_free": (None, [vp]),
         "shd_pe_tune": (C.c_int, [vp]),
+        "shd_pe_get_path": (C.c_int, [vp, i32, i32, vp, i32, vp]),
+        "shd_rowstore_foreach": (i64, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -350,6 +353,15 @@ class Engine:
             self.h, int(start), int(count), d_lat or None, d_rel or None, d_hops or None,
             d_flags or None), "shd_pe_copy_rows_device")
 
+    def get_path(self, src: int, dst: int, cap: int | None = None) -> list:
+        """shd_pe_get_path: the igraph shortest path [src, ..., dst] (vertex ids)."""
+        cap = cap or self.top.n + 1
+        buf = np.empty(cap, np.int32)
+        ln = C.c_int32(0)
+        self._chk(self._lib.shd_pe_get_path(self.h, int(src), int(dst), _p(buf), int(cap), C.byref(ln)),
+                  "shd_pe_get_path")
+        return buf[:ln.value].tolist()
+
     def tune(self):
         """shd_pe_tune: time both k_batch_rows variants on this engine's rows,
         keep the faster (leaves the table computed)."""
@@ -434,6 +446,18 @@ class RowStore:
             self.close()
         except Exception:
             pass
+
+    _VISIT = C.CFUNCTYPE(None, C.c_int32, C.c_int32, C.c_double, C.c_double, C.c_int32, C.c_uint64,
+                         C.c_void_p)
+
+    def items(self) -> list:
+        """shd_rowstore_foreach: every stored entry as (src, dst, lat, rel,
+        isDirect, packetCount) in the stored direction."""
+        out = []
+        cb = RowStore._VISIT(lambda s, d, lat, rel, isd, pc, u: out.append((s, d, lat, rel, isd, pc)))
+        n = self._lib.shd_rowstore_foreach(self.h, cb, None)
+        assert n == len(out)
+        return out
 
     def get(self, s, d):
         """(lat, rel, isDirect, packetCount) stored under exactly (s, d), or None."""

@@ -536,6 +536,59 @@ def test_tune_picks_a_variant_and_keeps_parity(E, oracle_mod):
     eng.close()
 
 
+def _oracle_path(top, og, s, t, att):
+    """igraph's path s -> t from the oracle's raw Dijkstra (parent edge ids)."""
+    _, par, _ = og.raw(int(s), att)
+    path, v = [int(t)], int(t)
+    while v != s:
+        e = int(par[v]) - 1
+        assert e >= 0, "unreached"
+        a, b = int(top.src[e]), int(top.dst[e])
+        v = a if (top.directed or b == v) else b
+        path.append(v)
+    return path[::-1]
+
+
+@pytest.mark.parametrize("case", ["tiefree", "quantized", "directed", "batched"])
+def test_get_path_matches_igraph(E, oracle_mod, case):
+    """shd_pe_get_path: the vertex sequence topology.c prints hop by hop
+    (:1449, :1502-1503) -- igraph's path, ties decided by its heap."""
+    if case == "directed":
+        top = G.random_sparse(700, 5, seed=31, directed=True)
+    elif case == "quantized":
+        top = G.random_sparse(800, 5, seed=32, quantum=0.5)
+    elif case == "batched":
+        top = G.power_law(3000, 3, seed=33, quantum=0.25)
+    else:
+        top = G.random_sparse(800, 5, seed=34)
+    att = np.arange(0, top.n, 3, dtype=np.int32)
+    eng = E.Engine(top, att, force_mode=5 if case == "batched" else 0)
+    og = oracle_mod.OracleGraph(top)
+    rng = np.random.default_rng(5)
+    checked = 0
+    for s in rng.choice(att, 4, replace=False):
+        for t in rng.choice(att, 6, replace=False):
+            if s == t:
+                assert eng.get_path(int(s), int(t)) == [int(s)]
+                continue
+            dist, _, _ = og.raw(int(s), att)
+            if dist[t] < 0:
+                with pytest.raises(E.EngineError):
+                    eng.get_path(int(s), int(t))
+                continue
+            got = eng.get_path(int(s), int(t))
+            assert got == _oracle_path(top, og, s, t, att), (case, s, t)
+            checked += 1
+        eng.compute_all()                 # invalidates the cached parent array
+    assert checked >= 10
+    s0, t0 = int(att[0]), int(att[-1])
+    with pytest.raises(E.EngineError):
+        eng.get_path(s0, t0, cap=1)
+    with pytest.raises(E.EngineError):
+        eng.get_path(s0, 1)               # vertex 1 is not attached
+    eng.close()
+
+
 def _twin_tie_graph(z_attached, seed=11):
     """A tie-free random graph plus twins a, b (both hanging off hub h with
     the same latency) and z adjacent to exactly a and b with equal latency:

@@ -75,6 +75,13 @@ def test_store_get_semantics_match_reference_cache(seed):
                 assert g == tuple(e)
     assert st.size() == sum(len(v) for v in ref.c.values())
     assert st.min_latency() == ref.min_lat
+    # the teardown dump (_topology_logAllCachedPaths, topology.c:1929-1967):
+    # every cached entry once, under the direction it was stored in
+    items = st.items()
+    assert len(items) == st.size()
+    want = {(s, d): tuple(e) for s, row in ref.c.items() for d, e in row.items()}
+    got = {(s, d): (lat, rel, bool(isd), pc) for s, d, lat, rel, isd, pc in items}
+    assert got == want
     # one slot per unordered pair at most, allocated per touched row
     assert st.memory_bytes() <= (k * (k + 1) // 2) * 25 + k * 8 + n * 4
 
