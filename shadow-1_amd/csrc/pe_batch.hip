@@ -134,6 +134,10 @@ template <> struct Bits<false> {
     __device__ __forceinline__ uint32_t ld(int w) const { return p[w]; }
     __device__ __forceinline__ void st(int w, uint32_t v) const { p[w] = v; }
     __device__ __forceinline__ void set(int v) const { atomicOr(&p[v >> 5], 1u << (v & 31)); }
+    // sets the bit, returns whether it was set before
+    __device__ __forceinline__ bool test_set(int v) const {
+        return (atomicOr(&p[v >> 5], 1u << (v & 31)) >> (v & 31)) & 1u;
+    }
 };
 template <> struct Bits<true> {
     uint32_t* p;
@@ -144,7 +148,25 @@ template <> struct Bits<true> {
     __device__ __forceinline__ void set(int v) const {
         __hip_atomic_fetch_or(&p[v >> 5], 1u << (v & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    __device__ __forceinline__ bool test_set(int v) const {
+        return (__hip_atomic_fetch_or(&p[v >> 5], 1u << (v & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP) >> (v & 31)) & 1u;
+    }
 };
+
+// Wave-aggregated append of `val` (lanes with `want`) to a list whose tail
+// counter lives in LDS: one LDS atomic per wave.
+__device__ __forceinline__ void wave_append(int32_t* Q, int* tail, bool want, int val) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(tail, __popcll(m));
+    base = __shfl(base, leader, 64);
+    if (want) __hip_atomic_store(&Q[base + __popcll(m & ((1ull << lane) - 1))], val, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // bucket of a key: the smallest multiple of delta above it
 __device__ __forceinline__ double next_bound(double mn, double delta) {
@@ -188,7 +210,14 @@ __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
     return acc;
 }
 
-template <int LB, int WPE, bool GB>
+// PART 0: the whole batch in one kernel (relax, predecessors over every
+// vertex, labels + writer, tie export).  PART 1 / 2: the same split in two
+// kernels over a round of batches whose dist arrays persist in HBM between
+// them (slot = batch index): PART 1 relaxes, PART 2 derives predecessors ON
+// DEMAND (only vertices on some target's path in some lane; the full pass only
+// for tie rows and trees too deep for the walks), labels, rows and the tie
+// export -- each with its own register budget.
+template <int LB, int WPE, bool GB, int PART>
 __global__ __launch_bounds__(BT_THREADS) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_batch_rows(DevGraph g0, DevTable tab0,
                                                            BatchScratch bs,
@@ -238,12 +267,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (b >= nBatches) break;
         const int row = batchRows[(size_t)b * LB + l];
         const int src = row >= 0 ? g.attached[row] : -1;
+        if constexpr (PART != 0) D = as_global(bs.D + (size_t)b * SE);
         // ---- init: dist = +inf (clean) for all (v, lane); pending sets empty ----
         {
             ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
             const size_t cnt2 = NE / 2;
             const ulonglong2 inf2 = make_ulonglong2(INF_ENC, INF_ENC);
-            for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
+            if constexpr (PART != 2)
+                for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
             for (int w = tid; w < nwp; w += NT) { any0.st(w, 0u); any1.st(w, 0u); }
             if (tid == 0) {
                 ctl->qtail = 0;
@@ -264,7 +295,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // key = dist + (maxOff - off) lines the lanes up behind the hub
         const double off = (row >= 0 && bs.rowOff) ? as_global(bs.rowOff)[row] : 0.0;
         if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
-        if (gid == 0 && src >= 0) {
+        if (PART != 2 && gid == 0 && src >= 0) {
             D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
             R[(size_t)src * LB + l] = 1.0;
             any0.set(src);
@@ -296,7 +327,22 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         long long procs = 0, arcsDone = 0, lanesAct = 0;
         double bound = delta;
         unsigned long long myFar = INF_BITS;      // smallest far key this thread added
+        if constexpr (PART == 2) failed = as_global(bs.flags)[b] != 0;
+        uint32_t needMask = 0u;
+        long long tPh2 = 0;
+        for (int attempt = 0;; ++attempt) {
+        const bool fullPred = PART != 2 || attempt > 0;
+        if (attempt > 0) {
+            if (tid == 0) {
+                ctl->qtail = 0;
+                ctl->changed = 0;
+                ctl->ambMask = 0u;
+            }
+            fence_wg();
+            __syncthreads();
+        }
         for (;;) {   // phases + verification until the Bellman check holds
+        if constexpr (PART != 2) {
         for (;;) {
             const Bits<GB> anyC = par ? any1 : any0;   // near
             const Bits<GB> anyF = par ? any0 : any1;   // far
@@ -563,7 +609,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             ++phases;
             __syncthreads();
         }
+        }   // PART != 2
         if (dbg) tPh1 = (long long)clock64();
+        if constexpr (PART == 1) break;
 
         // ================= 2. Bellman check + predecessor pass ===============
         // (a) every entry must satisfy dist[v] <= dist[u] + w for all in-arcs
@@ -576,14 +624,31 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         int viol = 0;
         {
             const Bits<GB> anyC = par ? any1 : any0;
-            for (int v0 = gid * BV; v0 < n; v0 += NG * BV) {
-                int a0[BV], a1[BV], ba[BV], cnt[BV], bu[BV];
+            // on demand: vertices are claimed in the (empty) far bitmap and
+            // listed in Q, targets first, then round by round the tree
+            // parents of the last round's entries in every lane
+            const Bits<GB> clm = par ? any0 : any1;
+            int lo = 0, hi = n;
+            if (!fullPred) {
+                for (int j = tid; j < g.T; j += NT) {
+                    const int v = g.attached[j];
+                    wave_append(Q, &ctl->qtail, !clm.test_set(v), v);
+                }
+                fence_wg();
+                __syncthreads();
+                hi = ctl->qtail;
+                __syncthreads();
+            }
+            while (lo < hi) {
+            for (int v0 = lo + gid * BV; v0 < hi; v0 += NG * BV) {
+                int a0[BV], a1[BV], ba[BV], cnt[BV], bu[BV], vx[BV];
                 unsigned long long dvb[BV], best[BV], mn[BV];
                 bool root[BV];
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    const int vv = v0 + v;
-                    if (vv < n) {
+                    const int vv = v0 + v < hi ? (fullPred ? v0 + v : ld_wg(&Q[v0 + v])) : -1;
+                    vx[v] = vv;
+                    if (vv >= 0) {
                         dvb[v] = dec(ld_wg(&D[(size_t)vv * LB + l]));
                         a0[v] = undirected ? g.rowPtr[vv] : g.inPtr[vv];
                         a1[v] = undirected ? g.rowPtr[vv + 1] : g.inPtr[vv + 1];
@@ -653,8 +718,8 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 }
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    const int vv = v0 + v;
-                    if (vv >= n) continue;
+                    const int vv = vx[v];
+                    if (vv < 0) continue;
                     const size_t e = (size_t)vv * LB + l;
                     const bool bad = !root[v] && mn[v] < dvb[v];
                     if (bad) {
@@ -681,7 +746,27 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const bool isSrc = vv == src;
                     H[e] = isSrc ? 0 : -1;
                     R[e] = isSrc ? 1.0 : -1.0;
+                    if (!tree) bu[v] = -1;
                 }
+                if (!fullPred) {
+                    // claim and list the parents (next round)
+#pragma unroll
+                    for (int v = 0; v < BV; ++v) {
+                        const int p = vx[v] >= 0 ? bu[v] : -1;
+                        wave_append(Q, &ctl->qtail, p >= 0 && !clm.test_set(p), p);
+                    }
+                }
+            }
+            if (fullPred) break;
+            fence_wg();
+            __syncthreads();
+            lo = hi;
+            hi = ctl->qtail;
+            __syncthreads();
+            }
+            if (!fullPred) {
+                for (int w = tid; w < nwp; w += NT) clm.st(w, 0u);
+                if (tid == 0) ctl->qtail = 0;
             }
         }
         if (viol) ctl->changed = 1;
@@ -695,9 +780,17 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         }
         __syncthreads();
         if (!anyViol || failed) break;
+        if constexpr (PART == 2) {   // no relaxation here to repair with: exact path
+            failed = true;
+            break;
+        }
         ++repairs;
         }   // verification loop
-        const long long tPh2 = dbg ? (long long)clock64() : 0;
+        if constexpr (PART == 1) {
+            if (tid == 0) as_global(bs.flags)[b] = failed ? 1 : 0;
+            break;
+        }
+        if (dbg) tPh2 = (long long)clock64();
 
         // ================= 3. labels on demand + row writer ==================
         // Only entries on some target's path need hops and reliability (27%
@@ -718,6 +811,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // O(depth^2 / SMAX)) switch to Gauss-Seidel sweeps over all entries
         // and a second writer pass.
         uint32_t relAmb = 0u;
+        bool retry = false;
         for (int pass = 0; pass < 2; ++pass) {
         bool deep = false;
         if (!failed && row >= 0) {
@@ -829,6 +923,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (tid == 0) ctl->changed = 0;
         __syncthreads();
         if (!anyDeep) break;
+        if (!fullPred) {         // the sweeps read every entry's parent
+            retry = true;
+            break;
+        }
         // Gauss-Seidel: every tree entry whose parent has labels takes them
         // (+1, * r) until a sweep changes nothing (<= depth sweeps).  These
         // entries were not walked, so an ambiguous one sends its row to the
@@ -869,9 +967,28 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         __syncthreads();
         // rows whose target paths meet an ambiguous entry (or that hit the
         // phase cap) go to k_exact_rows; their rows above are rewritten there
-        const uint32_t needMask = failed ? LBMASK : ctl->ambMask;
+        needMask = failed ? LBMASK : ctl->ambMask;
         __syncthreads();
         if (tid == 0) ctl->ambMask = 0u;
+        __syncthreads();
+        // a tie row's export needs every vertex's parent: the full pass
+        if (!fullPred && !failed && (retry || needMask)) continue;
+        break;
+        }   // attempts
+        if constexpr (PART == 1) {
+            if (dbg && tid == 0) {
+                dbg[16 * b + 0] = phases;
+                dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
+                dbg[16 * b + 15] = repairs;
+            }
+            if (dbg && l == 0 && procs) {
+                atomicAdd(&dbg[16 * b + 4], (int)procs);
+                atomicAdd(&dbg[16 * b + 9], (int)(arcsDone >> 4));
+                atomicAdd(&dbg[16 * b + 10], (int)lanesAct);
+            }
+            __syncthreads();
+            continue;
+        }
         const long long tPh3 = dbg ? (long long)clock64() : 0;
 
         // ---- tie export: hand k_exact_rows the final distances, the parents
@@ -930,12 +1047,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             rowAmbig[(size_t)b * LB + l] =
                 ((needMask >> l) & 1u) ? (uint8_t)(tieSlot[l] >= 0 ? 2 + tieSlot[l] : 1) : (uint8_t)0;
         if (dbg && tid == 0) {
-            dbg[16 * b + 0] = phases;
+            if (PART == 0) {
+                dbg[16 * b + 0] = phases;
+                dbg[16 * b + 15] = repairs;
+                dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
+            }
             dbg[16 * b + 1] = 0;
             dbg[16 * b + 2] = 0;
             dbg[16 * b + 3] = (int)needMask;
-            dbg[16 * b + 15] = repairs;
-            dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
             dbg[16 * b + 6] = (int)((tPh2 - tPh1) >> 10);
             dbg[16 * b + 7] = (int)((tPh3 - tPh2) >> 10);
             dbg[16 * b + 11] = (int)((tPh4 - tPh3) >> 10);
@@ -951,15 +1070,15 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     }
 }
 
-template <int LB, int WPE, bool GB>
+template <int LB, int WPE, bool GB, int PART>
 static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st,
                       int grid) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB, WPE, GB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB, WPE, GB, PART>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-    hipLaunchKernelGGL((k_batch_rows<LB, WPE, GB>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g, tab,
-                       bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
+    hipLaunchKernelGGL((k_batch_rows<LB, WPE, GB, PART>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g,
+                       tab, bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
 }
 
 int batch_lds_bytes(int n, int wpe, bool gbits) {
@@ -972,42 +1091,57 @@ int batch_lds_bytes(int n, int wpe, bool gbits) {
 
 int64_t batch_bits_words(int n) { return 2 * (int64_t)((((n + 31) >> 5) + 3) & ~3); }
 
-template <int WPE>
+template <int WPE, int PART>
 static const void* kptr(int lb, bool gb) {
-    if (gb) return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, true>);
-    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8, WPE, false>);
-    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32, WPE, false>);
-    return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, false>);
-}
-
-const void* batch_kernel_ptr(int lb, int wpe, bool gbits) {
-    return wpe >= 8 ? kptr<8>(lb, gbits) : kptr<4>(lb, gbits);
+    if (gb) return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, true, PART>);
+    if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8, WPE, false, PART>);
+    if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32, WPE, false, PART>);
+    return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, false, PART>);
 }
 
 template <int WPE>
+static const void* kptr_p(int lb, bool gb, int part) {
+    return part == 1 ? kptr<WPE, 1>(lb, gb) : part == 2 ? kptr<WPE, 2>(lb, gb) : kptr<WPE, 0>(lb, gb);
+}
+
+const void* batch_kernel_ptr(int lb, int wpe, bool gbits, int part) {
+    return wpe >= 8 ? kptr_p<8>(lb, gbits, part) : kptr_p<4>(lb, gbits, part);
+}
+
+template <int WPE, int PART>
 static void launch_w(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                      const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                      const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid) {
     if (cfg.gbits)    // graphs whose bitmaps exceed LDS: LB 16 only (the engine forces it)
-        launch_lb<16, WPE, true>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_lb<16, WPE, true, PART>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (cfg.lb == 8)
-        launch_lb<8, WPE, false>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_lb<8, WPE, false, PART>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (cfg.lb == 32)
-        launch_lb<32, WPE, false>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_lb<32, WPE, false, PART>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else
-        launch_lb<16, WPE, false>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_lb<16, WPE, false, PART>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+}
+
+template <int WPE>
+static void launch_wp(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
+                      const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
+                      const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid,
+                      int part) {
+    if (part == 1) launch_w<WPE, 1>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    else if (part == 2) launch_w<WPE, 2>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    else launch_w<WPE, 0>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
 }
 
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
-                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream) {
+                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream, int part) {
     if (nBatches <= 0) return;
     const int grid = nBatches < cfg.grid ? nBatches : cfg.grid;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (cfg.wpe >= 8)
-        launch_w<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_wp<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid, part);
     else
-        launch_w<4>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+        launch_wp<4>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid, part);
 }
 
 }  // namespace shdpe

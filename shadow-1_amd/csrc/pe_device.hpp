@@ -79,6 +79,7 @@ struct Tuning {
     int exactHc = 0, exactPerCU = 0;
     int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 1, batchWpe = 0;
     int relabel = 1;           // batched path: 1 = device ids by descending degree, 0 = as given
+    int batchSplit = 1;        // batched path: relax / post as two kernels (predecessors on demand)
     double batchDeltaFactor = 1.0, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
@@ -111,6 +112,7 @@ struct BatchScratch {
     int32_t* next;           // next batch to take (device counter, zeroed per launch)
     int64_t nStride;         // >= n, multiple of 64
     uint32_t* bits;          // [slot][2 * words] pending bitmaps when they exceed LDS (gbits)
+    int32_t* flags;          // split kernels: per batch of the round, 1 = phase cap hit
     const double* rowOff;    // [T] per table position: the source's distance to its
                              // batch hub (bucket key offset; null = no offsets)
 };
@@ -123,6 +125,7 @@ struct BatchLaunch {
     int32_t wpe;             // waves per SIMD the kernel variant is built for (4 or 8)
     double delta;            // bucket width
     int32_t gbits;           // 1: pending bitmaps in global scratch (n > ~655k vertices)
+    int32_t split;           // 1: relax and post as two kernels over rounds of batches
 };
 
 // Tie export (pe_batch.hip -> k_exact_rows early stop -> k_tie_write): per
@@ -200,8 +203,9 @@ void launch_path_walk(const DevGraph& g, const int32_t* dP, int32_t s, int32_t t
                       int32_t cap, int32_t* dLen, void* stream);
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
-                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream);
-const void* batch_kernel_ptr(int lb, int wpe, bool gbits);
+                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream,
+                       int part = 0);
+const void* batch_kernel_ptr(int lb, int wpe, bool gbits, int part = 0);
 int batch_lds_bytes(int n, int wpe, bool gbits);
 int64_t batch_bits_words(int n);   // per slot, both bitmaps
 // batched helpers (pe_aux.hip), all on `stream`

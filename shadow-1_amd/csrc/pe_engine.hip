@@ -69,6 +69,7 @@ struct Shard {
     bool tuned = false;
     BatchScratch bsc{};
     bool batchReady = false;
+    int32_t batchRound = 0;         // split kernels: batches per round (persisted dist arrays)
     int32_t* dBatchRows = nullptr;
     uint8_t* dBatchAmb = nullptr;
     TieBuf tie{};                   // early-stop tie rows (batched path)
@@ -158,6 +159,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_ORDER", t.batchOrder);
     gi("SHDPE_BATCH_WPE", t.batchWpe);
     gi("SHDPE_RELABEL", t.relabel);
+    gi("SHDPE_BATCH_SPLIT", t.batchSplit);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -313,6 +315,7 @@ static int configure(ShdPe* pe, Shard* sh) {
     if (pe->batched && !ok8 && !ok4) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
     const int first = forced ? forced : (ok8 ? 8 : 4);
+    v8.first.split = v4.first.split = tu.batchSplit ? 1 : 0;
     b = first == 8 ? v8.first : v4.first;
     sh->bcfgAlt = BatchLaunch{};
     if (!forced && ok8 && ok4) sh->bcfgAlt = first == 8 ? v4.first : v8.first;
@@ -805,13 +808,28 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->bcfg.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfg.grid);
     if (sh->bcfgAlt.grid > 0) sh->bcfgAlt.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt.grid);
     int rc;
-    void *D, *R, *H, *P, *q, *rows, *amb;
-    if ((rc = dev_alloc(sh, &D, slots * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
+    // split kernels: one persisted dist array per batch of a round (relax ->
+    // post), the rest per resident workgroup; rounds sized by free memory
+    // (at most 96 GiB of dist arrays: C4 one round of 13 GB, C5 two)
+    size_t roundB = slots;
+    if (sh->bcfg.split) {
+        size_t freeB = 0, totalB = 0;
+        if (hipMemGetInfo(&freeB, &totalB) != hipSuccess) freeB = (size_t)16 << 30;
+        const size_t perD = NS * LB * 8;
+        const size_t rest = slots * (perSlot - NS * LB * 8);
+        const size_t room = freeB > rest + ((size_t)12 << 30) ? freeB - rest - ((size_t)12 << 30) : perD;
+        const size_t dBudget = std::min<size_t>(room, (size_t)96 << 30);
+        roundB = std::max<size_t>(slots, std::min<size_t>(nBatchesAll, dBudget / perD));
+    }
+    sh->batchRound = (int32_t)roundB;
+    void *D, *R, *H, *P, *q, *rows, *amb, *fl;
+    if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
         (rc = dev_alloc(sh, &q, slots * NS * 4 + 64)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
-        (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)))
+        (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)) || (rc = dev_alloc(sh, &fl, roundB * 4 + 64)))
         return rc;
+    sh->bsc.flags = (int32_t*)fl;
     sh->bsc.D = (unsigned long long*)D;
     sh->bsc.R = (double*)R;
     sh->bsc.H = (int32_t*)H;
@@ -1033,8 +1051,23 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             if (sh->tie.cap > 0) HIPCHK(hipMemsetAsync(sh->tie.count, 0, 4, sh->stream));
             HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
-            launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
-                              sh->dDbg, sh->dTie, sh->stream);
+            if (!sh->bcfg.split) {
+                launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
+                                  sh->dDbg, sh->dTie, sh->stream, 0);
+            } else {
+                // rounds of batches: relax all of them, then the post kernel
+                // over the same batches (their dist arrays persist in HBM)
+                for (int32_t r0 = 0; r0 < nB; r0 += sh->batchRound) {
+                    const int32_t rn = std::min(sh->batchRound, nB - r0);
+                    const size_t ro = (size_t)r0 * LB;
+                    for (int part = 1; part <= 2; ++part) {
+                        HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
+                        launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows + ro, rn,
+                                          sh->dBatchAmb + ro, sh->bcfg, sh->dDbg ? sh->dDbg + 16 * r0 : nullptr,
+                                          sh->dTie, sh->stream, part);
+                    }
+                }
+            }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(sh->evB, sh->stream));
             amb.resize(order.size());
