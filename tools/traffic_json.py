@@ -26,34 +26,40 @@ KERNELS = ("k_batch_rows", "k_sparse_rows", "k_minplus", "k_direct_rows")
 def main():
     outdir, wl, tag = sys.argv[1], sys.argv[2], sys.argv[3]
     dst = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles", f"traffic_{wl}.json")
-    # per pass, only the LAST dispatch of each path kernel: bench.py runs
-    # shd_pe_tune (both kernel variants) before the measured step
-    last = {}
-    rows = defaultdict(list)
+    # per pass, only the measured step: the LAST dispatch of each path kernel
+    # (bench.py runs shd_pe_tune -- both kernel variants -- before it); the
+    # split batch path runs two kernels per step (k_batch_rows<.., 1> relax,
+    # <.., 2> post): the last post dispatch and the relax dispatch before it
+    per = defaultdict(list)          # (file, kernel family) -> [(dispatch, name, row)]
     for f in glob.glob(os.path.join(outdir, f"pmc_{wl}_*", "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = next((k for k in KERNELS if k in r.get("Kernel_Name", "")), None)
+            name = r.get("Kernel_Name", "")
+            k = next((k for k in KERNELS if k in name), None)
             if k is None:
                 continue
-            d = int(r.get("Dispatch_Id") or 0)
-            key = (f, k)
-            last[key] = max(last.get(key, -1), d)
-            rows[key].append((d, r))
+            per[(f, k)].append((int(r.get("Dispatch_Id") or 0), name, r))
     tot = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(lambda: defaultdict(set))
-    for (f, k), rs in rows.items():
-        for d, r in rs:
-            if d != last[(f, k)]:
-                continue
-            tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[k][r["Counter_Name"]].add((f, d))
+    for (f, k), rs in per.items():
+        ids = sorted({d for d, _, _ in rs})
+        last = ids[-1]
+        lastName = next(nm for d, nm, _ in rs if d == last)
+        keep = {last}
+        if ", 2>(" in lastName:
+            prev = [d for d, nm, _ in rs if d < last and ", 1>(" in nm]
+            if prev:
+                keep.add(max(prev))
+        for d, nm, r in rs:
+            if d in keep:
+                tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                disp[k][r["Counter_Name"]].add((f, d))
     if not tot:
         sys.exit(f"no counters for the path kernels under {outdir}/pmc_{wl}_*")
     k = max(tot, key=lambda x: tot[x].get("FETCH_SIZE", 0.0))
     c = tot[k]
     nl = max(1, len(disp[k].get("FETCH_SIZE", ())))
-    fetch = c.get("FETCH_SIZE", 0.0) * 1024 / nl
-    write = c.get("WRITE_SIZE", 0.0) * 1024 / max(1, len(disp[k].get("WRITE_SIZE", ())))
+    fetch = c.get("FETCH_SIZE", 0.0) * 1024      # one measured step (1 or 2 dispatches)
+    write = c.get("WRITE_SIZE", 0.0) * 1024
     hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
     from shdpe.engine import kernel_source_hash
     out = {
@@ -63,8 +69,9 @@ def main():
         "fetch_size_bytes": fetch,
         "write_bytes": write,
         "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
-        "launches_per_pass": nl,
-        "dispatch": "the last launch of the pass (the measured step; the tuning launches before it are ignored)",
+        "dispatches_per_step": nl,
+        "dispatch": "the measured step only: the last launch of the pass, with the relax launch before it "
+                    "when the batch path runs split (the tuning launches before them are ignored)",
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, KB*1024, "
                   "bench.py --steps 1 --warmup 0 (one launch).  Reads = 2 x FETCH_SIZE (gfx950 "
                   "calibration for random 128-B lines, profiles/r02e_fetch_calibration.json); "
