@@ -80,7 +80,7 @@ struct Tuning {
     int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 1, batchWpe = 0;
     int relabel = 1;           // batched path: 1 = device ids by descending degree, 0 = as given
     int batchSplit = 1;        // batched path: relax / post as two kernels (predecessors on demand)
-    double batchDeltaFactor = 1.0, batchScratchGB = 64.0;
+    double batchDeltaFactor = 0.75, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
     int debug = 0, streamWgPerCU = 16;
