@@ -1788,6 +1788,29 @@ __global__ __launch_bounds__(256) void k_stream_copy(const v4u* __restrict__ a,
     for (; i < n; i += stride) b[i] = a[i];
 }
 
+// one-pass shape: no grid-stride loop, one workgroup per 256 x UNR
+// elements (a grid of ~10^5 workgroups), UNR coalesced 4-KiB wave spans per
+// thread in flight before the stores
+template <bool NT, int UNR>
+__global__ __launch_bounds__(256) void k_stream_copy1(const v4u* __restrict__ a,
+                                                       v4u* __restrict__ b, size_t n) {
+    const size_t base = (size_t)blockIdx.x * 256 * UNR + threadIdx.x;
+    v4u x[UNR];
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+        const size_t i = base + (size_t)k * 256;
+        if (i < n) x[k] = NT ? __builtin_nontemporal_load(&a[i]) : a[i];
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+        const size_t i = base + (size_t)k * 256;
+        if (i < n) {
+            if (NT) __builtin_nontemporal_store(x[k], &b[i]);
+            else b[i] = x[k];
+        }
+    }
+}
+
 extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbps) {
     if (!pe || !gbps || bytes < (1 << 20) || iters < 1) return SHD_PE_EINVAL;
     Shard* sh = pe->shards[0].get();
@@ -1801,15 +1824,28 @@ extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, 
     if (hipMemsetAsync(a, 0, n * 16, sh->stream) != hipSuccess) rc = SHD_PE_EHIP;
     // shapes: cache policy (plain / non-temporal) x 4 or 8 loads in flight per
     // thread x workgroups per CU (SHDPE_STREAM_WG_PER_CU adds one more)
+    // plus the one-pass shape (shapes 12..19: policy x 4 / 8 / 2 / 1 per
+    // thread; nt with 4 per thread is the best on the boxes seen, ~6.1 TB/s)
     const int wgs[3] = {4, 8, pe->tu.streamWgPerCU};
-    for (int shape = 0; shape < 12 && !rc; ++shape) {
+    for (int shape = 0; shape < 20 && !rc; ++shape) {
         const bool nt = shape & 1;
-        const int unr = (shape >> 1) & 1 ? 8 : 4;
-        const int grid = sh->numCUs * wgs[shape >> 2];
+        const bool onePass = shape >= 12;
+        const int unr = shape >= 18 ? 1 : shape >= 16 ? 2 : (shape >> 1) & 1 ? 8 : 4;
+        const int grid = onePass ? (int)((n + 256 * (size_t)unr - 1) / (256 * (size_t)unr))
+                                 : sh->numCUs * wgs[shape >> 2];
         auto launch = [&]() {
             const v4u* pa = (const v4u*)a;
             v4u* pb = (v4u*)b;
-            if (nt && unr == 8) hipLaunchKernelGGL((k_stream_copy<true, 8>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+            if (onePass) {
+                if (unr == 2 && nt) hipLaunchKernelGGL((k_stream_copy1<true, 2>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+                else if (unr == 2) hipLaunchKernelGGL((k_stream_copy1<false, 2>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+                else if (unr == 1 && nt) hipLaunchKernelGGL((k_stream_copy1<true, 1>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+                else if (unr == 1) hipLaunchKernelGGL((k_stream_copy1<false, 1>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+                else if (nt && unr == 8) hipLaunchKernelGGL((k_stream_copy1<true, 8>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+                else if (nt) hipLaunchKernelGGL((k_stream_copy1<true, 4>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+                else if (unr == 8) hipLaunchKernelGGL((k_stream_copy1<false, 8>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+                else hipLaunchKernelGGL((k_stream_copy1<false, 4>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
+            } else if (nt && unr == 8) hipLaunchKernelGGL((k_stream_copy<true, 8>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
             else if (nt) hipLaunchKernelGGL((k_stream_copy<true, 4>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
             else if (unr == 8) hipLaunchKernelGGL((k_stream_copy<false, 8>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
             else hipLaunchKernelGGL((k_stream_copy<false, 4>), dim3(grid), dim3(256), 0, sh->stream, pa, pb, n);
@@ -1824,7 +1860,11 @@ extern "C" int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, 
         }
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, sh->evA, sh->evB);
-        if (ms > 0.f) best = std::max(best, 2.0 * (double)n * 16.0 * iters / (ms * 1e-3) / 1e9);
+        const double gb = ms > 0.f ? 2.0 * (double)n * 16.0 * iters / (ms * 1e-3) / 1e9 : 0.0;
+        if (pe->tu.debug)
+            std::fprintf(stderr, "[shdpe] stream shape %d (%s, %d per thread, grid %d): %.0f GB/s\n", shape,
+                         nt ? "nt" : "plain", unr, grid, gb);
+        best = std::max(best, gb);
     }
     if (!rc) *gbps = best;
     (void)hipFree(a);
