@@ -266,6 +266,7 @@ def main():
         "tie_row_fraction": st["rowsExact"] / max(1, args.steps * count),
         "ms_exact_per_step": st["msExactKernel"] / max(1, args.steps),
         "batch_kernel_waves": st["batchWaves"] or None,
+        "batch_post_kernel_waves": st["batchPostWaves"] or None,
     }
     if rank == 0 and not args.no_stream:
         sbw = eng.stream_bandwidth()     # 16-B streaming copy kernel, same device

@@ -136,7 +136,10 @@ typedef struct ShdPeStats {
                                   kernel exported distances, parents and the tie
                                   threshold; k_tie_write wrote the row)          */
     int32_t batchWaves;        /* k_batch_rows variant in use: waves per SIMD (4
-                                  or 8; shd_pe_tune picks the faster)             */
+                                  or 8; shd_pe_tune picks the faster); with the
+                                  split kernels, the relaxation kernel's          */
+    int32_t batchPostWaves;    /* split kernels: the post kernel's variant (the
+                                  tune times relax and post separately)           */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */

@@ -50,6 +50,7 @@ struct Shard {
     hipStream_t stream = nullptr;
     hipStream_t copyStream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evA = nullptr, evB = nullptr;
+    hipEvent_t evP[3] = {nullptr, nullptr, nullptr};   // per-part timing (shd_pe_tune)
     std::vector<void*> allocs;
     DevGraph dg{};                  // path kernels (device ids, possibly relabelled)
     DevGraph dgAux{};               // caller's ids, rows sorted by id (aux kernels)
@@ -66,7 +67,11 @@ struct Shard {
     int exactGrid = 0, exactHc = 1;
     BatchLaunch bcfg{};
     BatchLaunch bcfgAlt{};          // the other kernel variant (grid 0: none), shd_pe_tune
+    BatchLaunch bcfgPost{};         // split kernels: post-kernel variant when the tune picked
+                                    // another one than bcfg's (grid 0: bcfg)
     bool tuned = false;
+    bool timeParts = false;         // split kernels: time relax / post launches (tune)
+    double msPart[2] = {0.0, 0.0};
     BatchScratch bsc{};
     bool batchReady = false;
     int32_t batchRound = 0;         // split kernels: batches per round (persisted dist arrays)
@@ -325,6 +330,7 @@ static int configure(ShdPe* pe, Shard* sh) {
     sh->stats.batched = pe->batched ? 1 : 0;
     sh->stats.batchLanes = pe->batched ? b.lb : 0;
     sh->stats.batchWaves = pe->batched ? b.wpe : 0;
+    sh->stats.batchPostWaves = pe->batched && b.split ? b.wpe : 0;
     return SHD_PE_OK;
 }
 
@@ -438,7 +444,7 @@ static void destroy_shard(Shard* s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     if (s->comm) (void)ncclCommDestroy(s->comm);
     for (void* p : s->allocs) (void)hipFree(p);
-    for (hipEvent_t e : {s->ev0, s->ev1, s->evA, s->evB})
+    for (hipEvent_t e : {s->ev0, s->ev1, s->evA, s->evB, s->evP[0], s->evP[1], s->evP[2]})
         if (e) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->copyStream) (void)hipStreamDestroy(s->copyStream);
@@ -587,7 +593,9 @@ static int init_shard(ShdPe* pe, Shard* sh) {
     if (hipStreamCreateWithFlags(&sh->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&sh->copyStream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&sh->ev0) != hipSuccess || hipEventCreate(&sh->ev1) != hipSuccess ||
-        hipEventCreate(&sh->evA) != hipSuccess || hipEventCreate(&sh->evB) != hipSuccess)
+        hipEventCreate(&sh->evA) != hipSuccess || hipEventCreate(&sh->evB) != hipSuccess ||
+        hipEventCreate(&sh->evP[0]) != hipSuccess || hipEventCreate(&sh->evP[1]) != hipSuccess ||
+        hipEventCreate(&sh->evP[2]) != hipSuccess)
         return SHD_PE_ENODEV;
     int rc = configure(pe, sh);
     if (rc) return rc;
@@ -1057,14 +1065,23 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             } else {
                 // rounds of batches: relax all of them, then the post kernel
                 // over the same batches (their dist arrays persist in HBM)
+                // (the post kernel may run another variant: bcfgPost)
+                const BatchLaunch& post = sh->bcfgPost.grid > 0 ? sh->bcfgPost : sh->bcfg;
                 for (int32_t r0 = 0; r0 < nB; r0 += sh->batchRound) {
                     const int32_t rn = std::min(sh->batchRound, nB - r0);
                     const size_t ro = (size_t)r0 * LB;
+                    if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[0], sh->stream));
                     for (int part = 1; part <= 2; ++part) {
                         HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
                         launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows + ro, rn,
-                                          sh->dBatchAmb + ro, sh->bcfg, sh->dDbg ? sh->dDbg + 16 * r0 : nullptr,
-                                          sh->dTie, sh->stream, part);
+                                          sh->dBatchAmb + ro, part == 1 ? sh->bcfg : post,
+                                          sh->dDbg ? sh->dDbg + 16 * r0 : nullptr, sh->dTie, sh->stream, part);
+                        if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[part], sh->stream));
+                    }
+                    if (sh->timeParts) {
+                        HIPCHK(hipEventSynchronize(sh->evP[2]));
+                        sh->msPart[0] += elapsed(sh->evP[0], sh->evP[1]);
+                        sh->msPart[1] += elapsed(sh->evP[1], sh->evP[2]);
                     }
                 }
             }
@@ -1241,29 +1258,44 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
         std::vector<int32_t> pos(sh->rowCount);
         for (int32_t i = 0; i < sh->rowCount; ++i) pos[i] = sh->rowStart + i;
         const ShdPeStats keep = sh->stats;
-        double ms[2] = {0.0, 0.0};
+        double ms[2] = {0.0, 0.0}, part[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
         int w[2] = {0, 0};
+        const BatchLaunch cand[2] = {sh->bcfg, sh->bcfgAlt};
+        sh->bcfgPost = BatchLaunch{};
         for (int k = 0; k < 2; ++k) {
+            sh->bcfg = cand[k];
             w[k] = sh->bcfg.wpe;
             // a first launch of each variant maps its code and scratch; the
-            // second is timed
+            // second is timed (split kernels: relax and post separately)
             for (int rep = 0; rep < 2; ++rep) {
                 const double m0 = sh->stats.msSparseKernel;
+                sh->msPart[0] = sh->msPart[1] = 0.0;
+                sh->timeParts = rep == 1 && sh->bcfg.split;
                 int rc = compute_shard(pe, sh, pos.data(), sh->rowCount);
-                if (rc) { sh->stats = keep; return rc; }
+                sh->timeParts = false;
+                if (rc) { sh->bcfg = cand[0]; sh->bcfgAlt = cand[1]; sh->stats = keep; return rc; }
                 ms[k] = sh->stats.msSparseKernel - m0;
+                part[k][0] = sh->msPart[0];
+                part[k][1] = sh->msPart[1];
             }
-            std::swap(sh->bcfg, sh->bcfgAlt);
         }
-        // ms[0]: the starting variant, ms[1]: the alternative (now in bcfgAlt
-        // again after the second swap)
-        if (ms[1] < ms[0]) std::swap(sh->bcfg, sh->bcfgAlt);
+        // whole launches, or per part when both variants ran split: the
+        // relax kernel and the post kernel each take their faster variant
+        const bool perPart = cand[0].split && cand[1].split && part[0][0] > 0.0 && part[1][0] > 0.0;
+        const int rk = perPart ? (part[1][0] < part[0][0] ? 1 : 0) : (ms[1] < ms[0] ? 1 : 0);
+        const int pk = perPart ? (part[1][1] < part[0][1] ? 1 : 0) : rk;
+        sh->bcfg = cand[rk];
+        sh->bcfgAlt = cand[1 - rk];
+        if (pk != rk) sh->bcfgPost = cand[pk];
         sh->tuned = true;
         sh->stats = keep;
         sh->stats.batchWaves = sh->bcfg.wpe;
+        sh->stats.batchPostWaves = sh->bcfg.split ? cand[pk].wpe : 0;
         if (pe->tu.debug)
-            std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms, %d waves %.2f ms -> %d\n",
-                         sh->gindex, w[0], ms[0], w[1], ms[1], sh->bcfg.wpe);
+            std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms (relax %.2f post %.2f), "
+                         "%d waves %.2f ms (relax %.2f post %.2f) -> relax %d, post %d waves\n",
+                         sh->gindex, w[0], ms[0], part[0][0], part[0][1], w[1], ms[1], part[1][0],
+                         part[1][1], sh->bcfg.wpe, cand[pk].wpe);
     }
     return SHD_PE_OK;
 }
@@ -1948,6 +1980,7 @@ extern "C" int shd_pe_reset_stats(ShdPe* pe) {
         st.batched = keep.batched;
         st.batchLanes = keep.batchLanes;
         st.batchWaves = keep.batchWaves;
+        st.batchPostWaves = keep.batchPostWaves;
     }
     pe->msGather = 0.0;
     return SHD_PE_OK;

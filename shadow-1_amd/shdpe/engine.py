@@ -68,7 +68,8 @@ class Stats(C.Structure):
                 ("msDenseKernel", C.c_double), ("launchesDense", C.c_int64),
                 ("denseSweeps", C.c_int64), ("denseFlops", C.c_double),
                 ("batched", C.c_int32), ("batchLanes", C.c_int32), ("nShards", C.c_int32),
-                ("msGather", C.c_double), ("rowsTieEarly", C.c_int64), ("batchWaves", C.c_int32)]
+                ("msGather", C.c_double), ("rowsTieEarly", C.c_int64), ("batchWaves", C.c_int32),
+                ("batchPostWaves", C.c_int32)]
 
 
 class EngineError(RuntimeError):
