@@ -1115,6 +1115,21 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 std::vector<int32_t> dbg((size_t)nB * 16);
                 HIPCHK(hipMemcpy(dbg.data(), sh->dDbg, dbg.size() * 4, hipMemcpyDeviceToHost));
                 print_batch_debug(pe, sh, dbg.data(), nB);
+                // SHDPE_DUMP_BATCHES=<file>: per batch its rows (table
+                // positions, -1 pads), hub offsets and kernel counters, for
+                // offline batch-cost models (tools/batch_cost.py)
+                if (const char* f = std::getenv("SHDPE_DUMP_BATCHES")) {
+                    if (FILE* fp = std::fopen(f, "wb")) {
+                        const int32_t hdr[2] = {nB, LB};
+                        std::fwrite(hdr, 4, 2, fp);
+                        std::fwrite(order.data(), 4, order.size(), fp);
+                        std::fwrite(dbg.data(), 4, dbg.size(), fp);
+                        const int64_t nOff = (int64_t)pe->rowOff.size();
+                        std::fwrite(&nOff, 8, 1, fp);
+                        std::fwrite(pe->rowOff.data(), 8, pe->rowOff.size(), fp);
+                        std::fclose(fp);
+                    }
+                }
             }
         } else {
             if ((rc = ensure_tie(pe, sh))) return rc;
