@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4")
     ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--sub-shards", type=int, default=1,
+                    help="row shards per GPU, computed concurrently on their own streams")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
@@ -123,11 +125,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # BENCH_REHEARSE_ONE_GPU=1: rehearse the N-rank flow on a one-GPU box
+    # (every rank's shard engine on cuda:0, gloo for the barrier and the
+    # max-over-ranks reduction); the driver's multi-GPU runs use RCCL
+    rehearse = os.environ.get("BENCH_REHEARSE_ONE_GPU") == "1"
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            local = 0
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from shdpe import generators as G
     from shdpe.engine import Engine, DEBUG_ENV
@@ -135,7 +145,8 @@ def main():
     # SHDPE_* tuning variables reach the library only through its debug flag
     dbg = DEBUG_ENV if any(k.startswith("SHDPE_") for k in os.environ) else 0
     top, att = G.make_config(args.workload)
-    eng = Engine(top, att, device=local, shard_index=rank, shard_count=world, debug_flags=dbg)
+    eng = Engine(top, att, device=local, shard_index=rank, shard_count=world, debug_flags=dbg,
+                 devices=[local] * args.sub_shards if args.sub_shards > 1 else None)
     T = eng.T
     start, count = eng.owned
     st0 = eng.stats()
@@ -165,7 +176,7 @@ def main():
     st = eng.stats()
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
