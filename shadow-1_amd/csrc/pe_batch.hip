@@ -48,8 +48,8 @@ constexpr int BK = 4;        // arcs per vertex per load batch
 // 1024-thread workgroup per CU, two vertices interleaved per group) or 8
 // (64 VGPRs, two workgroups per CU, one vertex per group)
 template <int WPE> struct BCfg {
-    static constexpr int BV = WPE >= 8 ? 1 : 2;      // vertices interleaved per group
-    static constexpr int SMAX = WPE >= 8 ? 8 : 16;   // label-walk stack: (entry, arc) pairs per thread
+    static constexpr int BV = WPE >= 6 ? 1 : 2;      // vertices interleaved per group
+    static constexpr int SMAX = WPE >= 6 ? 8 : 16;   // label-walk stack: (entry, arc) pairs per thread
 };
 constexpr int WALK_BUDGET = 2048;   // walk steps per target before the deep-tree sweeps
 // Lane policy of the relaxation: a vertex with ANY dirty lane below the
@@ -1081,10 +1081,12 @@ static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch
                        tab, bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
 }
 
+int batch_threads(int wpe) { return wpe == 6 ? 768 : BT_THREADS; }
+
 int batch_lds_bytes(int n, int wpe, bool gbits) {
     const int nwp = (((n + 31) >> 5) + 3) & ~3;
     // label walks reuse the relax bitmaps' LDS for their stacks
-    const int stack = BT_THREADS * (wpe >= 8 ? BCfg<8>::SMAX : BCfg<4>::SMAX) * 8;
+    const int stack = batch_threads(wpe) * (wpe >= 6 ? BCfg<8>::SMAX : BCfg<4>::SMAX) * 8;
     const int bits = gbits ? 0 : 2 * 4 * nwp;
     return 64 + (bits > stack ? bits : stack);
 }
@@ -1105,7 +1107,8 @@ static const void* kptr_p(int lb, bool gb, int part) {
 }
 
 const void* batch_kernel_ptr(int lb, int wpe, bool gbits, int part) {
-    return wpe >= 8 ? kptr_p<8>(lb, gbits, part) : kptr_p<4>(lb, gbits, part);
+    return wpe >= 8 ? kptr_p<8>(lb, gbits, part) : wpe == 6 ? kptr_p<6>(lb, gbits, part)
+                                                             : kptr_p<4>(lb, gbits, part);
 }
 
 template <int WPE, int PART>
@@ -1140,6 +1143,8 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (cfg.wpe >= 8)
         launch_wp<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid, part);
+    else if (cfg.wpe == 6)
+        launch_wp<6>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid, part);
     else
         launch_wp<4>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid, part);
 }

@@ -207,6 +207,7 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
                        int part = 0);
 const void* batch_kernel_ptr(int lb, int wpe, bool gbits, int part = 0);
 int batch_lds_bytes(int n, int wpe, bool gbits);
+int batch_threads(int wpe);    // workgroup size of a variant (6 waves: 768, else 1024)
 int64_t batch_bits_words(int n);   // per slot, both bitmaps
 // batched helpers (pe_aux.hip), all on `stream`
 void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, int64_t nEdges,

@@ -67,6 +67,7 @@ struct Shard {
     int exactGrid = 0, exactHc = 1;
     BatchLaunch bcfg{};
     BatchLaunch bcfgAlt{};          // the other kernel variant (grid 0: none), shd_pe_tune
+    BatchLaunch bcfgAlt2{};         // a third variant (6 waves), shd_pe_tune
     BatchLaunch bcfgPost{};         // split kernels: post-kernel variant when the tune picked
                                     // another one than bcfg's (grid 0: bcfg)
     bool tuned = false;
@@ -286,14 +287,14 @@ static int configure(ShdPe* pe, Shard* sh) {
     // control block, else in each slot's global scratch (gbits, LB 16)
     b.gbits = pe->batched && batch_lds_bytes((int)n, 8, false) > LDS ? 1 : 0;
     if (b.gbits) b.lb = 16;
-    auto occupancy = [&](int wpe) {
+    auto occupancy = [&](int wpe, int threads) {
         const int lds = batch_lds_bytes((int)n, wpe, b.gbits != 0);
         int per = 0;
         if (lds > LDS ||
             hipFuncSetAttribute(batch_kernel_ptr(b.lb, wpe, b.gbits != 0),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, batch_kernel_ptr(b.lb, wpe, b.gbits != 0),
-                                                         b.threads, lds) != hipSuccess)
+                                                         threads, lds) != hipSuccess)
             per = 0;
         return per;
     };
@@ -306,24 +307,28 @@ static int configure(ShdPe* pe, Shard* sh) {
     auto make = [&](int wpe) {
         BatchLaunch c = b;
         c.wpe = wpe;
+        if (wpe == 6) c.threads = batch_threads(6);   // two 768-thread workgroups per CU
         c.ldsBytes = batch_lds_bytes((int)n, wpe, b.gbits != 0);
-        const int per = c.ldsBytes <= LDS ? occupancy(wpe) : 0;
+        const int per = c.ldsBytes <= LDS ? occupancy(wpe, c.threads) : 0;
         c.grid = sh->numCUs * std::max(per, 1);
         if (tu.batchGrid > 0 && tu.batchGrid < c.grid) c.grid = tu.batchGrid;
         c.delta = pe->opt.delta > 0 ? pe->opt.delta : g.meanArcLatency * tu.batchDeltaFactor;
         if (!(c.delta > 0)) c.delta = 1.0;
         return std::make_pair(c, per);
     };
-    const int forced = tu.batchWpe == 4 || tu.batchWpe == 8 ? tu.batchWpe : 0;
-    auto v8 = make(8), v4 = make(4);
-    const bool ok8 = v8.second >= 1, ok4 = v4.second >= 1;
+    const int forced = tu.batchWpe == 4 || tu.batchWpe == 6 || tu.batchWpe == 8 ? tu.batchWpe : 0;
+    auto v8 = make(8), v4 = make(4), v6 = make(6);
+    const bool ok8 = v8.second >= 1, ok4 = v4.second >= 1, ok6 = v6.second >= 2 && b.threads == 1024;
     if (pe->batched && !ok8 && !ok4) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
-    const int first = forced ? forced : (ok8 ? 8 : 4);
-    v8.first.split = v4.first.split = tu.batchSplit ? 1 : 0;
-    b = first == 8 ? v8.first : v4.first;
-    sh->bcfgAlt = BatchLaunch{};
+    const int first = forced == 6 && ok6 ? 6 : forced == 4 || !ok8 ? 4 : 8;
+    v8.first.split = v4.first.split = v6.first.split = tu.batchSplit ? 1 : 0;
+    b = first == 8 ? v8.first : first == 6 ? v6.first : v4.first;
+    sh->bcfgAlt = sh->bcfgAlt2 = BatchLaunch{};
     if (!forced && ok8 && ok4) sh->bcfgAlt = first == 8 ? v4.first : v8.first;
+    // the 6-wave variant (768 threads: 80 VGPRs, fewer spills than 8 waves'
+    // 64) joins the tune when two of its workgroups fit a CU
+    if (!forced && ok6 && tu.batchSplit) sh->bcfgAlt2 = v6.first;
     (void)need0;
     sh->bcfg = b;
     sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
@@ -811,10 +816,11 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
     const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
-    const size_t grid = (size_t)std::max(sh->bcfg.grid, sh->bcfgAlt.grid);
+    const size_t grid = (size_t)std::max({sh->bcfg.grid, sh->bcfgAlt.grid, sh->bcfgAlt2.grid});
     const size_t slots = std::min<size_t>({grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
     sh->bcfg.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfg.grid);
     if (sh->bcfgAlt.grid > 0) sh->bcfgAlt.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt.grid);
+    if (sh->bcfgAlt2.grid > 0) sh->bcfgAlt2.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt2.grid);
     int rc;
     // split kernels: one persisted dist array per batch of a round (relax ->
     // post), the rest per resident workgroup; rounds sized by free memory
@@ -1269,15 +1275,19 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
     std::lock_guard<std::mutex> lk(pe->mu);
     for (auto& sp : pe->shards) {
         Shard* sh = sp.get();
-        if (sh->tuned || sh->bcfgAlt.grid <= 0 || sh->rowCount <= 0) continue;
+        if (sh->tuned || (sh->bcfgAlt.grid <= 0 && sh->bcfgAlt2.grid <= 0) || sh->rowCount <= 0) continue;
         std::vector<int32_t> pos(sh->rowCount);
         for (int32_t i = 0; i < sh->rowCount; ++i) pos[i] = sh->rowStart + i;
         const ShdPeStats keep = sh->stats;
-        double ms[2] = {0.0, 0.0}, part[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-        int w[2] = {0, 0};
-        const BatchLaunch cand[2] = {sh->bcfg, sh->bcfgAlt};
+        double ms[3] = {0.0, 0.0, 0.0}, part[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+        int w[3] = {0, 0, 0};
+        BatchLaunch cand[3] = {sh->bcfg, sh->bcfgAlt, sh->bcfgAlt2};
+        const BatchLaunch orig[3] = {sh->bcfg, sh->bcfgAlt, sh->bcfgAlt2};
+        int nc = 1;
+        if (sh->bcfgAlt.grid > 0) cand[nc++] = sh->bcfgAlt;
+        if (sh->bcfgAlt2.grid > 0) cand[nc++] = sh->bcfgAlt2;
         sh->bcfgPost = BatchLaunch{};
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < nc; ++k) {
             sh->bcfg = cand[k];
             w[k] = sh->bcfg.wpe;
             // a first launch of each variant maps its code and scratch; the
@@ -1288,29 +1298,37 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
                 sh->timeParts = rep == 1 && sh->bcfg.split;
                 int rc = compute_shard(pe, sh, pos.data(), sh->rowCount);
                 sh->timeParts = false;
-                if (rc) { sh->bcfg = cand[0]; sh->bcfgAlt = cand[1]; sh->stats = keep; return rc; }
+                if (rc) {
+                    sh->bcfg = orig[0]; sh->bcfgAlt = orig[1]; sh->bcfgAlt2 = orig[2];
+                    sh->stats = keep;
+                    return rc;
+                }
                 ms[k] = sh->stats.msSparseKernel - m0;
                 part[k][0] = sh->msPart[0];
                 part[k][1] = sh->msPart[1];
             }
         }
-        // whole launches, or per part when both variants ran split: the
-        // relax kernel and the post kernel each take their faster variant
-        const bool perPart = cand[0].split && cand[1].split && part[0][0] > 0.0 && part[1][0] > 0.0;
-        const int rk = perPart ? (part[1][0] < part[0][0] ? 1 : 0) : (ms[1] < ms[0] ? 1 : 0);
-        const int pk = perPart ? (part[1][1] < part[0][1] ? 1 : 0) : rk;
+        // whole launches, or per part when every variant ran split: the
+        // relax kernel and the post kernel each take their fastest variant
+        bool perPart = true;
+        for (int k = 0; k < nc; ++k) perPart = perPart && cand[k].split && part[k][0] > 0.0;
+        int rk = 0, pk = 0;
+        for (int k = 1; k < nc; ++k) {
+            if (perPart ? part[k][0] < part[rk][0] : ms[k] < ms[rk]) rk = k;
+            if (perPart ? part[k][1] < part[pk][1] : ms[k] < ms[pk]) pk = k;
+        }
+        if (!perPart) pk = rk;
         sh->bcfg = cand[rk];
-        sh->bcfgAlt = cand[1 - rk];
         if (pk != rk) sh->bcfgPost = cand[pk];
         sh->tuned = true;
         sh->stats = keep;
         sh->stats.batchWaves = sh->bcfg.wpe;
         sh->stats.batchPostWaves = sh->bcfg.split ? cand[pk].wpe : 0;
         if (pe->tu.debug)
-            std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms (relax %.2f post %.2f), "
-                         "%d waves %.2f ms (relax %.2f post %.2f) -> relax %d, post %d waves\n",
-                         sh->gindex, w[0], ms[0], part[0][0], part[0][1], w[1], ms[1], part[1][0],
-                         part[1][1], sh->bcfg.wpe, cand[pk].wpe);
+            for (int k = 0; k < nc; ++k)
+                std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms (relax %.2f post %.2f)%s\n",
+                             sh->gindex, w[k], ms[k], part[k][0], part[k][1],
+                             k == nc - 1 ? (pk == rk ? " -> one variant" : " -> per part") : "");
     }
     return SHD_PE_OK;
 }

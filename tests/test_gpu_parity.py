@@ -524,7 +524,8 @@ def test_tune_picks_a_variant_and_keeps_parity(E, oracle_mod):
     eng = E.Engine(top, att, force_mode=5)
     eng.tune()
     st = eng.stats()
-    assert st["batched"] == 1 and st["batchWaves"] in (4, 8) and st["rowsComputed"] == 0
+    assert st["batched"] == 1 and st["batchWaves"] in (4, 6, 8) and st["rowsComputed"] == 0
+    assert st["batchPostWaves"] in (4, 6, 8)
     og = oracle_mod.OracleGraph(top)
     pos = np.arange(0, eng.T, 97)
     exp = og.rows(eng.attached[pos], eng.attached, threads=8)
@@ -534,6 +535,25 @@ def test_tune_picks_a_variant_and_keeps_parity(E, oracle_mod):
             _assert_rows_equal(got, {k: v[i] for k, v in exp.items()}, f"round {rnd} row {p}")
         eng.compute_all()
     eng.close()
+
+
+@pytest.mark.parametrize("wpe", [4, 6, 8])
+@pytest.mark.parametrize("case", ["power_law", "quantized"])
+def test_batched_kernel_each_variant(E, oracle_mod, monkeypatch, wpe, case):
+    """Every k_batch_rows variant the tune may pick (4 / 6 / 8 waves per
+    SIMD; 6 = two 768-thread workgroups per CU) forced through
+    SHDPE_BATCH_WPE, bit-exact with the oracle, tie rows included."""
+    monkeypatch.setenv("SHDPE_BATCH_WPE", str(wpe))
+    if case == "power_law":
+        top = G.power_law(8000, m=3, seed=14)
+        att = G.sample_attached(top.n, 1200, seed=3)
+        srcs = att[::5]
+    else:
+        top, att, srcs = G.random_sparse(600, 6, seed=214, quantum=1.0), np.arange(600), None
+    st = _check_engine(E, oracle_mod, top, att, sources=srcs, force=5, debug_flags=E.DEBUG_ENV)
+    assert st["batched"] == 1 and st["batchWaves"] == wpe
+    if case == "quantized":
+        assert st["rowsExact"] > 0
 
 
 def _oracle_path(top, og, s, t, att):
