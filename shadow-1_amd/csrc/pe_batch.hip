@@ -229,6 +229,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     constexpr int SMAX = BCfg<WPE>::SMAX;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int tieSlot[LB];
+    __shared__ int laneRow[LB];           // table row of each lane (-1: pad)
     __shared__ unsigned long long tieThr[LB];
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
@@ -267,6 +268,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (b >= nBatches) break;
         const int row = batchRows[(size_t)b * LB + l];
         const int src = row >= 0 ? g.attached[row] : -1;
+        if (gid == 0) laneRow[l] = row;
         if constexpr (PART != 0) D = as_global(bs.D + (size_t)b * SE);
         // ---- init: dist = +inf (clean) for all (v, lane); pending sets empty ----
         {
@@ -817,32 +819,15 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (!failed && row >= 0) {
             int2* const stk = reinterpret_cast<int2*>(smem + 64);
             const int T = (int)tab.T;
-            const size_t base = (size_t)(row - tab.rowStart) * (size_t)tab.T;
             // pass 0: the deep-tree budget; pass 1: only the never-spin net
             // (every consistent entry is resolved by then)
             const long long stepCap = pass == 0 ? (long long)WALK_BUDGET : 4LL * n + 64;
             for (int j = gid; j < T; j += NG) {
                 const int t = g.attached[j];
-                double L = 0.0, Rl = 0.0;
-                int h = -1, pv = -1;
-                uint8_t f = 0;
-                if (t == src) {
-                    // 1-vertex igraph path [s]: the fold uses edge (s,s)
-                    // (:1469-1488); the destination factor is skipped (:1457)
-                    if (g.hasSelf[src]) {
-                        L = 0.0 + g.selfLat[src];
-                        Rl = (1.0 * g.vrel[src]) * g.selfRel[src];
-                        h = 1;
-                    } else {
-                        f |= F_NOEDGE;
-                    }
-                } else {
+                if (t != src) {
                     const size_t e = (size_t)t * LB + l;
                     const unsigned long long dt = dec(ld_wg(&D[e]));
-                    if (dt == INF_BITS) {
-                        f |= F_UNREACHABLE;
-                    } else {
-                        L = b2d(dt);
+                    if (dt != INF_BITS) {
                         int he = ld_wg(&H[e]);
                         double re = ld_wg(&R[e]);
                         long long steps = 0;
@@ -894,25 +879,8 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             }
                             cur = (int)e;           // top segment resolved: walk again
                         }
-                        h = he;
-                        const int pa = ld_wg(&P[e]);
-                        pv = pa >= 0 ? g.inCol[pa & ~TIE_AMB] : -1;
-                        if (pv >= 0 && g.oldId) pv = g.oldId[pv];   // device id -> caller's id
-                        if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
-                            Rl = re;
-                        else
-                            Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
-                        if (L == 0.0) {                 // topology.c:1848-1852
-                            L = 1.0;
-                            f |= F_ZEROLAT;
-                        }
                     }
                 }
-                tab.lat[base + j] = L;
-                tab.rel[base + j] = Rl;
-                tab.hops[base + j] = h;
-                tab.flags[base + j] = f;
-                if (tab.pred) tab.pred[base + j] = pv;
             }
         }
         if (deep) ctl->changed = 1;
@@ -961,7 +929,82 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
             if (!any) break;
         }
-        }   // writer passes
+        }   // label passes
+        // ---- row writer: the lanes' rows are written target block by
+        // target block through an LDS tile (the walk stacks' space): a
+        // group holds one target of 16 rows, so direct stores would scatter
+        // 16 rows x 8-32 B per wave instruction; from the tile each wave
+        // stores a run of consecutive columns of one row (non-temporal:
+        // the table is never re-read here)
+        if (!failed && !retry) {
+            const int T = (int)tab.T;
+            double* const tLat = reinterpret_cast<double*>(smem + 64);
+            double* const tRel = tLat + NT;
+            int32_t* const tHop = reinterpret_cast<int32_t*>(tRel + NT);
+            int32_t* const tPred = tHop + NT;
+            uint8_t* const tFlg = reinterpret_cast<uint8_t*>(tPred + NT);
+            const int wl = tid / NG, wc = tid % NG;     // writer: lane (row), column in block
+            const int wrow = laneRow[wl];
+            const size_t wbase = (size_t)(wrow >= 0 ? wrow - tab.rowStart : 0) * (size_t)tab.T;
+            __syncthreads();                            // walks done: stacks free
+            for (int j0 = 0; j0 < T; j0 += NG) {
+                const int j = j0 + gid;
+                double L = 0.0, Rl = 0.0;
+                int h = -1, pv = -1;
+                uint8_t f = 0;
+                if (row >= 0 && j < T) {
+                    const int t = g.attached[j];
+                    if (t == src) {
+                        // 1-vertex igraph path [s]: the fold uses edge (s,s)
+                        // (:1469-1488); the destination factor is skipped (:1457)
+                        if (g.hasSelf[src]) {
+                            L = 0.0 + g.selfLat[src];
+                            Rl = (1.0 * g.vrel[src]) * g.selfRel[src];
+                            h = 1;
+                        } else {
+                            f |= F_NOEDGE;
+                        }
+                    } else {
+                        const size_t e = (size_t)t * LB + l;
+                        const unsigned long long dt = dec(ld_wg(&D[e]));
+                        if (dt == INF_BITS) {
+                            f |= F_UNREACHABLE;
+                        } else {
+                            L = b2d(dt);
+                            h = ld_wg(&H[e]);
+                            const int pa = ld_wg(&P[e]);
+                            pv = pa >= 0 ? g.inCol[pa & ~TIE_AMB] : -1;
+                            if (pv >= 0 && g.oldId) pv = g.oldId[pv];   // device id -> caller's id
+                            if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
+                                Rl = ld_wg(&R[e]);
+                            else
+                                Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
+                            if (L == 0.0) {                 // topology.c:1848-1852
+                                L = 1.0;
+                                f |= F_ZEROLAT;
+                            }
+                        }
+                    }
+                }
+                const int ti = l * NG + gid;
+                tLat[ti] = L;
+                tRel[ti] = Rl;
+                tHop[ti] = h;
+                tPred[ti] = pv;
+                tFlg[ti] = f;
+                __syncthreads();
+                if (wrow >= 0 && j0 + wc < T) {
+                    const int ti2 = wl * NG + wc;
+                    const size_t o = wbase + (size_t)(j0 + wc);
+                    __builtin_nontemporal_store(tLat[ti2], &tab.lat[o]);
+                    __builtin_nontemporal_store(tRel[ti2], &tab.rel[o]);
+                    __builtin_nontemporal_store(tHop[ti2], &tab.hops[o]);
+                    __builtin_nontemporal_store(tFlg[ti2], &tab.flags[o]);
+                    if (tab.pred) __builtin_nontemporal_store(tPred[ti2], &tab.pred[o]);
+                }
+                __syncthreads();
+            }
+        }
         if (relAmb) atomicOr(&ctl->ambMask, 1u << l);
         fence_wg();
         __syncthreads();

@@ -31,7 +31,7 @@ for st in ${STAGES:-tests bench}; do
           L=shadow-1_amd/libshdpe.so; [ $lib != new ] && L=shadow-1_amd/libshdpe_$lib.so
           SHDPE_LIB=$R/$L timeout -k 10 300 python3 -u bench.py --workload $wl --steps 3 --warmup 1 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > $OUT/ab_${wl}_$lib.json 2> $OUT/ab_${wl}_$lib.err || { tail -20 $OUT/ab_${wl}_$lib.err; exit 1; }
           line $OUT/ab_${wl}_$lib.json "$wl $lib #$rep"
-          [ -n "$ABDEBUG" ] && { SHDPE_LIB=$R/$L SHDPE_DEBUG=1 timeout -k 10 300 python3 -u bench.py --workload $wl --steps 1 --warmup 0 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > /dev/null 2> $OUT/abdbg_${wl}_$lib.err || exit 1; grep shdpe $OUT/abdbg_${wl}_$lib.err | head -8; }
+          if [ -n "$ABDEBUG" ]; then SHDPE_LIB=$R/$L SHDPE_DEBUG=1 timeout -k 10 300 python3 -u bench.py --workload $wl --steps 1 --warmup 0 --no-cpu --tie-stress "" --d2h-rows 0 --no-stream > /dev/null 2> $OUT/abdbg_${wl}_$lib.err || exit 1; grep shdpe $OUT/abdbg_${wl}_$lib.err | head -8; fi
         done
       done
     done ;;
