@@ -135,8 +135,8 @@ typedef struct ShdPeStats {
     int64_t rowsTieEarly;      /* of rowsExact: early-stop emulation (the batch
                                   kernel exported distances, parents and the tie
                                   threshold; k_tie_write wrote the row)          */
-    int32_t batchWaves;        /* k_batch_rows variant in use: waves per SIMD (4
-                                  or 8; shd_pe_tune picks the faster); with the
+    int32_t batchWaves;        /* k_batch_rows variant in use: waves per SIMD (4,
+                                  6 or 8; shd_pe_tune picks the faster); with the
                                   split kernels, the relaxation kernel's          */
     int32_t batchPostWaves;    /* split kernels: the post kernel's variant (the
                                   tune times relax and post separately)           */
@@ -170,9 +170,10 @@ int shd_pe_attached(const ShdPe* pe, int32_t* outVertices);
 int shd_pe_compute_all(ShdPe* pe);
 
 /* Optional, once, before timed or production use: computes the engine's
- * own rows with each k_batch_rows variant (8 / 4 waves per SIMD) and keeps
- * the faster for later calls (their ranking differs between boxes of the
- * same SKU).  The table is left fully computed; no-op on other paths. */
+ * own rows with each k_batch_rows variant (8 / 6 / 4 waves per SIMD; the
+ * relax and post kernels are timed separately and each keeps its faster
+ * variant) for later calls (the ranking differs between boxes of the same
+ * SKU).  The table is left fully computed; no-op on other paths. */
 int shd_pe_tune(ShdPe* pe);
 
 /* Compute rows for the given sources (vertex ids, must be attached). */
