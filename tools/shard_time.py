@@ -14,6 +14,7 @@ for N in [int(x) for x in sys.argv[2:]]:
     eng = Engine(top, att, shard_index=0, shard_count=N, debug_flags=dbg)
     s0, cnt = eng.owned
     pos = np.arange(s0, s0 + cnt, dtype=np.int32)
+    eng.tune()                               # as bench.py: per-box kernel variants
     eng.compute_positions(s0, cnt)           # warm-up (allocations)
     best = 1e9
     for _ in range(3):
@@ -24,6 +25,7 @@ for N in [int(x) for x in sys.argv[2:]]:
         best = min(best, time.perf_counter() - t)
     st = eng.stats()
     print(f"{wl} N={N} rows={cnt} ms={best*1e3:.1f} lanes={st['batchLanes']} "
+          f"waves={st['batchWaves']}/{st['batchPostWaves']} "
           f"rows/s/gpu={cnt/best:.0f} -> {N*cnt/best:.0f} total "
           f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('SHDPE_'))}]", flush=True)
     eng.close()
