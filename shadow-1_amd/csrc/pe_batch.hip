@@ -190,18 +190,18 @@ template <int LB>
 __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
                                               const double* __restrict__ inRel,
                                               const int32_t* __restrict__ inCol,
-                                              const Lab* L, int l, int s, int t, int h) {
+                                              const int32_t* P, int l, int s, int t, int h) {
     // (arrays by value: a DevGraph& would pin the caller's descriptor in scratch)
     double acc = 1.0 * vrel[s];
     acc = acc * vrel[t];
     for (int lo = 0; lo < h; lo += 64) {        // hops (lo, hi] counted from the source
         const int hi = min(h, lo + 64);
         int x = t;
-        for (int up = 0; up < h - hi; ++up) x = inCol[ld_wg(&L[(size_t)x * LB + l].p) & ~TIE_AMB];
+        for (int up = 0; up < h - hi; ++up) x = inCol[ld_wg(&P[(size_t)x * LB + l]) & ~TIE_AMB];
         double fac[64];
         int k = 0;
         while (k < hi - lo) {
-            const int a = ld_wg(&L[(size_t)x * LB + l].p) & ~TIE_AMB;
+            const int a = ld_wg(&P[(size_t)x * LB + l]) & ~TIE_AMB;
             fac[k++] = inRel[a];
             x = inCol[a];
         }
@@ -253,7 +253,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const size_t NS = (size_t)bs.nStride;
     const size_t SE = NS * LB;
     unsigned long long* D = as_global(bs.D + slot * SE);
-    Lab* LBL = as_global(bs.lab + slot * SE);
+    double* R = as_global(bs.R + slot * SE);
+    int32_t* H = as_global(bs.H + slot * SE);
+    int32_t* P = as_global(bs.P + slot * SE);
     int32_t* Q = as_global(bs.queue + slot * NS);
 
     // batches are taken from a device counter (dynamic: a batch's cost varies
@@ -297,7 +299,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
         if (PART != 2 && gid == 0 && src >= 0) {
             D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
-            LBL[(size_t)src * LB + l].r = 1.0;
+            R[(size_t)src * LB + l] = 1.0;
             any0.set(src);
         }
         fence_wg();
@@ -742,12 +744,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     // parent the heap decides; labels unresolved (-1) except
                     // at the source (hops 0, rel 1: the fold's start)
                     const int hx = tree ? ba[v] : -1;
+                    P[e] = ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx;
                     const bool isSrc = vv == src;
-                    Lab lb;
-                    lb.p = ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx;
-                    lb.h = isSrc ? 0 : -1;
-                    lb.r = isSrc ? 1.0 : -1.0;
-                    LBL[e] = lb;
+                    H[e] = isSrc ? 0 : -1;
+                    R[e] = isSrc ? 1.0 : -1.0;
                     if (!tree) bu[v] = -1;
                 }
                 if (!fullPred) {
@@ -828,8 +828,8 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const size_t e = (size_t)t * LB + l;
                     const unsigned long long dt = dec(ld_wg(&D[e]));
                     if (dt != INF_BITS) {
-                        int he = ld_wg(&LBL[e].h);
-                        double re = ld_wg(&LBL[e].r);
+                        int he = ld_wg(&H[e]);
+                        double re = ld_wg(&R[e]);
                         long long steps = 0;
                         int cur = (int)e;
                         while (!(he >= 0 && re >= 0.0)) {
@@ -837,7 +837,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             double rp = 0.0;
                             bool found = false;
                             while (sp < SMAX) {
-                                const int a = ld_wg(&LBL[x].p);
+                                const int a = ld_wg(&P[x]);
                                 if (a < 0 || ++steps > stepCap) {
                                     if (a >= 0 && pass == 0) deep = true;   // -> sweeps
                                     else relAmb = 1u;      // no parent / a cycle: exact path
@@ -850,8 +850,8 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 stk[sp * NT + tid] = make_int2(x, arc);
                                 ++sp;
                                 const int pe = g.inCol[arc] * LB + l;
-                                const int hq = ld_wg(&LBL[pe].h);
-                                const double rq = ld_wg(&LBL[pe].r);
+                                const int hq = ld_wg(&H[pe]);
+                                const double rq = ld_wg(&R[pe]);
                                 if (hq >= 0 && rq >= 0.0) {
                                     hp = hq;
                                     rp = rq;
@@ -868,8 +868,8 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 const int2 sx = stk[i * NT + tid];
                                 hp += 1;
                                 rp = rp * g.inRel[sx.y];
-                                st_wg(&LBL[sx.x].h, hp);
-                                st_wg(&LBL[sx.x].r, rp);
+                                st_wg(&H[sx.x], hp);
+                                st_wg(&R[sx.x], rp);
                             }
                             if (sp == 0) break;     // gave up (deep / inconsistent)
                             if (cur == (int)e) {
@@ -903,19 +903,19 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         for (int sweep = 0; sweep <= n + 1; ++sweep) {
             int ch = 0;
             for (size_t e = tid; e < NE; e += NT) {
-                const int a = ld_wg(&LBL[e].p);
+                const int a = ld_wg(&P[e]);
                 if (a < 0) continue;
                 const int ll = (int)(e % LB);
                 const int arc = a & ~TIE_AMB;
                 const int pe = g.inCol[arc] * LB + ll;
-                const int hq = ld_wg(&LBL[pe].h);
-                const double rq = ld_wg(&LBL[pe].r);
+                const int hq = ld_wg(&H[pe]);
+                const double rq = ld_wg(&R[pe]);
                 if (hq < 0 || rq < 0.0) continue;
                 const int hn = hq + 1;
                 const double rn = rq * g.inRel[arc];
-                if (ld_wg(&LBL[e].h) != hn || ld_wg(&LBL[e].r) != rn) {
-                    st_wg(&LBL[e].h, hn);
-                    st_wg(&LBL[e].r, rn);
+                if (ld_wg(&H[e]) != hn || ld_wg(&R[e]) != rn) {
+                    st_wg(&H[e], hn);
+                    st_wg(&R[e], rn);
                     ch = 1;
                     if (a & TIE_AMB) atomicOr(&ctl->ambMask, 1u << ll);
                 }
@@ -971,14 +971,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             f |= F_UNREACHABLE;
                         } else {
                             L = b2d(dt);
-                            h = ld_wg(&LBL[e].h);
-                            const int pa = ld_wg(&LBL[e].p);
+                            h = ld_wg(&H[e]);
+                            const int pa = ld_wg(&P[e]);
                             pv = pa >= 0 ? g.inCol[pa & ~TIE_AMB] : -1;
                             if (pv >= 0 && g.oldId) pv = g.oldId[pv];   // device id -> caller's id
                             if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
-                                Rl = ld_wg(&LBL[e].r);
+                                Rl = ld_wg(&R[e]);
                             else
-                                Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, LBL, l, src, t, h);
+                                Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
                             if (L == 0.0) {                 // topology.c:1848-1852
                                 L = 1.0;
                                 f |= F_ZEROLAT;
@@ -1056,7 +1056,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             for (int v = gid; v < n; v += NG) {
                 if (sl < 0) continue;
                 const size_t e = (size_t)v * LB + l;
-                const int pe = ld_wg(&LBL[e].p);
+                const int pe = ld_wg(&P[e]);
                 const bool am = pe >= 0 && (pe & TIE_AMB);
                 const size_t o = (size_t)sl * (size_t)tie.n + v;
                 tie.D[o] = b2d(dec(ld_wg(&D[e])));

@@ -103,18 +103,11 @@ struct DevScratch {
 // workgroup; every per-vertex array is [n][LB] (LB sources of the batch
 // side by side, so one arc relaxation serves LB sources with one coalesced
 // access).
-// Per (vertex, lane) labels of the batch kernel's post pass, one 16-B record
-// so a label walk step reads one sector (parent arc, hops, rel product)
-// instead of three lines of three arrays.
-struct alignas(16) Lab {
-    int32_t p;               // chosen IN-arc (| TIE_AMB), -1 none
-    int32_t h;               // hop label (-1 unresolved)
-    double r;                // rel product label (< 0 unresolved)
-};
-
 struct BatchScratch {
     unsigned long long* D;   // [slot][nStride][LB] f64 bit patterns (dist)
-    Lab* lab;                // [slot][nStride][LB] labels
+    double* R;               // [slot][nStride][LB] rel product label (< 0 unresolved)
+    int32_t* H;              // [slot][nStride][LB] hop label (-1 unresolved)
+    int32_t* P;              // [slot][nStride][LB] chosen IN-arc (| TIE_AMB), -1 none
     int32_t* queue;          // [slot][nStride] phase candidate list
     int32_t* next;           // next batch to take (device counter, zeroed per launch)
     int64_t nStride;         // >= n, multiple of 64
