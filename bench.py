@@ -97,9 +97,110 @@ def load_traffic(workload):
     return None
 
 
+def roofline_of(st, n, m_arcs, T, count):
+    """Roofline of the dominant kernel from the engine's own HIP-event kernel
+    times (stats), algorithmic work per SURVEY.md §8(d): sparse rows
+    12*m_arcs + 12*n + 20*T bytes each (HBM), direct rows 36*T bytes each
+    (HBM), dense min-plus 2 flops per executed relaxation (FP64 VALU)."""
+    ms_kernel = st["msSparseKernel"] + st["msDirectKernel"] + st["msDenseKernel"]
+    launches = max(1, st["launchesSparse"] + st["launchesDirect"] + st["launchesDense"])
+    avg_launch_ms = ms_kernel / launches
+    bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+    if st["mode"] == 2:
+        work = 36 * T * count
+        kname = "k_direct_rows"
+        achieved = work / (avg_launch_ms * 1e-3) / 1e9
+    elif st["mode"] == 3:
+        # dense min-plus: SURVEY §8d prices a sweep at 2*n^2 flops per row;
+        # sweeps skip K chunks that cannot improve (chunk epochs), so the
+        # work counted is what the kernels executed: visited (row tile, K
+        # chunk) pairs x 2 flops per relaxation, + the pred pass
+        work = st["denseFlops"] / max(1, st["launchesDense"])
+        kname = "k_minplus"
+        bound, unit, peak = "valu-fp64", "TFLOP/s", FP64_VALU_PEAK_TF
+        achieved = work / (avg_launch_ms * 1e-3) / 1e12
+    else:
+        work = algorithmic_bytes_per_row(n, m_arcs, T) * count
+        kname = "k_batch_rows" if st["batched"] else "k_sparse_rows"
+        achieved = work / (avg_launch_ms * 1e-3) / 1e9
+    return {"bound": bound, "kernel": kname, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "algorithmic_per_launch": work,
+            "avg_launch_ms": avg_launch_ms, "launches": launches}
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """--gpus N > 1 without a launcher: start N fresh rank processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env), before
+    this process touches the GPU or torch.cuda.  Rank 0's stdout (the JSON
+    line) is relayed; the first child to fail takes the others down and its
+    exit code is returned.  No exec: the children are ordinary subprocesses."""
+    import signal
+    import subprocess
+    import threading
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=subprocess.PIPE if r == 0 else None))
+
+    def relay(p):
+        for line in iter(p.stdout.readline, b""):
+            sys.stdout.write(line.decode(errors="replace"))
+            sys.stdout.flush()
+    th = threading.Thread(target=relay, args=(procs[0],), daemon=True)
+    th.start()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the others\n")
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.2)
+            if rc:
+                t0 = time.time()
+                while any(q.poll() is None for q in live) and time.time() - t0 < 20:
+                    time.sleep(0.2)
+                for q in live:
+                    if q.poll() is None:
+                        q.kill()
+                for q in live:
+                    q.wait()
+                live = []
+    th.join(timeout=10)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without a launcher's WORLD_SIZE this "
+                         "process starts the N rank processes itself")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launcher self-test: every rank prints its rank env as JSON and exits")
+    ap.add_argument("--secondary", default="c3a,c5",
+                    help="comma list of further configs timed after the headline (rank 0, N=1; "
+                         "'' = off): ms_per_step, rows/s and roofline of each")
+    ap.add_argument("--host-fill", type=int, default=1,
+                    help="time the end-to-end host fill (compute + rows into pinned buffers + "
+                         "shd_rowstore_store_row for every row) once after the timed region")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4")
@@ -113,7 +214,7 @@ def main():
                          "share is 16 CPUs, os.cpu_count() there shows the whole machine)")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the device-copy HBM bandwidth reference")
-    ap.add_argument("--tie-stress", default="c2q,c4q,c5q",
+    ap.add_argument("--tie-stress", default="c2q,c4q,c5q,c3bq",
                     help="comma list of quantised variants timed after the headline (rank 0, "
                          "N=1; '' = off): their tie-row fraction and k_exact_rows time")
     ap.add_argument("--d2h-rows", type=int, default=2048,
@@ -121,9 +222,29 @@ def main():
                          "region (PCIe-inclusive rate, reported separately; 0 = off)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to "
+                         f"report a {world}-rank run as {args.gpus} GPUs\n")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_launch:
+        sys.stdout.write(json.dumps({"rank": rank, "local_rank": local, "world": world,
+                                     "master": f"{os.environ.get('MASTER_ADDR')}:"
+                                               f"{os.environ.get('MASTER_PORT')}",
+                                     "pid": os.getpid()}) + "\n")   # one write: no interleaving
+        sys.stdout.flush()
+        # launcher self-test hooks: one rank fails, the others hang
+        if os.environ.get("BENCH_DRY_FAIL_RANK") == str(rank):
+            sys.exit(3)
+        if os.environ.get("BENCH_DRY_FAIL_RANK"):
+            time.sleep(120)
+        return
     dist = None
     # BENCH_REHEARSE_ONE_GPU=1: rehearse the N-rank flow on a one-GPU box
     # (every rank's shard engine on cuda:0, gloo for the barrier and the
@@ -222,27 +343,9 @@ def main():
 
     rows_total = T * args.steps
     value = rows_total / elapsed
-    ms_kernel = st["msSparseKernel"] + st["msDirectKernel"] + st["msDenseKernel"]
-    launches = max(1, st["launchesSparse"] + st["launchesDirect"] + st["launchesDense"])
-    avg_launch_ms = ms_kernel / launches
-    bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
-    if st["mode"] == 2:
-        bytes_per_launch = 36 * T * count
-        kname = "k_direct_rows"
-        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    elif st["mode"] == 3:
-        # dense min-plus: FP64 VALU roof.  SURVEY §8d prices a sweep at 2*n^2
-        # flops per row; sweeps skip K chunks that cannot improve (chunk
-        # epochs), so the work counted is what the kernels executed: visited
-        # (row tile, K chunk) pairs x 2 flops per relaxation, + the pred pass
-        bytes_per_launch = st["denseFlops"] / max(1, st["launchesDense"])
-        kname = "k_minplus"
-        bound, unit, peak = "valu-fp64", "TFLOP/s", FP64_VALU_PEAK_TF
-        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e12
-    else:
-        bytes_per_launch = algorithmic_bytes_per_row(n, m_arcs, T) * count
-        kname = "k_batch_rows" if st["batched"] else "k_sparse_rows"
-        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    rl = roofline_of(st, n, m_arcs, T, count)
+    bound, bytes_per_launch, achieved, avg_launch_ms = (rl["bound"], rl["algorithmic_per_launch"],
+                                                        rl["achieved"], rl["avg_launch_ms"])
     traffic = load_traffic(args.workload)
     traffic_bytes = (traffic or {}).get("bytes_per_launch")
     if traffic_bytes and count != T:
@@ -267,16 +370,12 @@ def main():
                    "sources": T, "targets": T, "rows_per_step": T,
                    "parallelism": f"source-row shards x{world}"},
         "edges_relaxed_per_s": m_arcs * rows_total / elapsed,
-        "roofline": {"bound": bound, "kernel": kname, "achieved": achieved,
-                     "peak": peak, "unit": unit, "frac": achieved / peak,
-                     "traffic": traffic_bytes,
-                     "traffic_tag": (traffic or {}).get("tag"),
-                     "algorithmic_per_launch": bytes_per_launch,
-                     "avg_launch_ms": avg_launch_ms, "launches": launches},
+        "roofline": dict(rl, traffic=traffic_bytes, traffic_tag=(traffic or {}).get("tag")),
         "rows_exact": st["rowsExact"] // max(1, args.steps),
         "tie_row_fraction": st["rowsExact"] / max(1, args.steps * count),
         "ms_exact_per_step": st["msExactKernel"] / max(1, args.steps),
         "batch_kernel_waves": st["batchWaves"] or None,
+        "batch_lanes": st["batchLanes"] or None,
         "batch_post_kernel_waves": st["batchPostWaves"] or None,
     }
     if rank == 0 and not args.no_stream:
@@ -303,7 +402,11 @@ def main():
             allc = cpu_baseline(top, att, budget_s=args.cpu_budget / 2, threads=args.cpu_threads)
             out["cpu_baseline_all_cores"] = allc
             out["speedup_vs_cpu_all_cores"] = value / allc["value"]
+    if rank == 0 and world == 1 and args.host_fill:
+        out["host_fill"] = host_fill(eng, top)
     eng.close()
+    if rank == 0 and world == 1 and args.secondary:
+        out["secondary"] = [secondary(wl, args.steps, dbg) for wl in args.secondary.split(",") if wl]
     if rank == 0 and world == 1 and args.tie_stress:
         out["tie_stress"] = [tie_stress(wl, args.steps, dbg) for wl in args.tie_stress.split(",") if wl]
     if rank == 0:
@@ -311,6 +414,97 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def secondary(workload, steps, dbg):
+    """Another BASELINE config timed the same way as the headline (setup and
+    tune untimed, rows resident in HBM): ms per full table, rows/s and the
+    roofline of its dominant kernel (C3a: k_direct_rows, HBM; C5:
+    k_batch_rows, HBM; C3b: k_minplus, FP64 VALU)."""
+    from shdpe import generators as G
+    from shdpe.engine import Engine
+    g0 = time.perf_counter()
+    top, att = G.make_config(workload)
+    eng = Engine(top, att, debug_flags=dbg)
+    setup_s = time.perf_counter() - g0
+    st0 = eng.stats()
+    eng.tune()
+    eng.compute_all()                        # warm-up
+    eng.synchronize()
+    eng.reset_stats()
+    k = max(1, min(steps, 3))
+    t0 = time.perf_counter()
+    for _ in range(k):
+        eng.compute_all()
+    eng.synchronize()
+    el = (time.perf_counter() - t0) / k
+    st = eng.stats()
+    T = eng.T
+    out = {"workload": workload, "desc": G.CONFIGS.get(workload, {}).get("desc"),
+           "vertices": st0["nVertices"], "arcs": st0["nArcs"], "rows": int(T), "steps": k,
+           "ms_per_step": el * 1e3, "rows_per_s": T / el,
+           "edges_relaxed_per_s": st0["nArcs"] * T / el,
+           "roofline": roofline_of(st, st0["nVertices"], st0["nArcs"], T, T),
+           "tie_rows": st["rowsExact"] // k, "ms_exact_per_step": st["msExactKernel"] / k,
+           "batch_lanes": st["batchLanes"] or None, "setup_s": setup_s}
+    eng.close()
+    return out
+
+
+def host_fill(eng, top, block=1024, threads=0):
+    """End-to-end path-cache fill as the drop-in does it (topology.c:1805-1864
+    for every row): one more compute, then rows DMA'd in blocks into
+    page-locked buffers (shd_pe_get_rows into shd_pe_host_alloc memory,
+    lat / rel / flags) and stored with shd_rowstore_store_rows, the next
+    block's copy overlapping the current block's store.  Outside `value`."""
+    import threading
+    from shdpe.engine import RowStore
+    T = eng.T
+    start, count = eng.owned
+    eng.synchronize()
+    t0 = time.perf_counter()
+    eng.compute_all()
+    eng.synchronize()
+    t_gpu = time.perf_counter() - t0
+    store = RowStore(top.n, eng.attached)
+    fields = ("lat", "rel", "flags")
+    bufs = [eng.pinned_rows(min(block, count), fields) for _ in range(2)]
+    blocks = [(b0, min(block, count - b0)) for b0 in range(0, count, block)]
+    d2h_s, store_s = [0.0], 0.0
+    res = []
+
+    def fetch(i, buf):
+        b0, c = blocks[i]
+        f0 = time.perf_counter()
+        eng.get_rows(start + b0, c, out=buf)
+        d2h_s[0] += time.perf_counter() - f0
+
+    f0 = time.perf_counter()
+    th = threading.Thread(target=fetch, args=(0, bufs[0]))
+    th.start()
+    for i, (b0, c) in enumerate(blocks):
+        th.join()
+        if i + 1 < len(blocks):
+            th = threading.Thread(target=fetch, args=(i + 1, bufs[(i + 1) % 2]))
+            th.start()
+        b = bufs[i % 2]
+        s0 = time.perf_counter()
+        res.append(store.store_rows(eng.attached[start + b0:start + b0 + c], b["lat"], b["rel"],
+                                    b["flags"], threads=threads))
+        store_s += time.perf_counter() - s0
+    fill_s = time.perf_counter() - f0
+    out = {"rows": int(count), "block_rows": block, "ms_compute": t_gpu * 1e3,
+           "ms_fill": fill_s * 1e3, "ms_d2h_sum": d2h_s[0] * 1e3, "ms_store_sum": store_s * 1e3,
+           "host_fill_rows_per_s": count / (t_gpu + fill_s),
+           "end_to_end_over_compute": (t_gpu + fill_s) / t_gpu,
+           "entries_stored": int(store.size()), "store_GB": store.memory_bytes() / 1e9,
+           "rows_all_success": int(sum(int(r.sum()) for r in res)),
+           "how": "compute_all + shd_pe_get_rows into shd_pe_host_alloc buffers (lat, rel, flags) "
+                  "+ shd_rowstore_store_rows (threads by slot rows), copy of block b+1 overlapping "
+                  "the store of block b"}
+    store.close()
+    del bufs
+    return out
 
 
 def tie_stress(workload, steps, dbg):

@@ -337,6 +337,19 @@ int shd_rowstore_store(ShdRowStore* st, int32_t s, int32_t d, int32_t isDirect,
  * is an edge.  Returns 1 if every target succeeded, 0 if not, < 0 error. */
 int shd_rowstore_store_row(ShdRowStore* st, int32_t s, const double* lat, const double* rel,
                            const uint8_t* flags, int32_t isComplete, const uint8_t* adjacent);
+/* The whole-table fill: `count` engine rows at once (row i of source srcs[i]
+ * at lat/rel/flags/adjacent + i * ld, ld >= nAttached -- e.g. a block of
+ * shd_pe_get_rows output in shd_pe_host_alloc buffers), with exactly the
+ * result of shd_rowstore_store_row on srcs[0], srcs[1], ... in order
+ * (topology.c:1805-1864 once per row, in the order Shadow's first misses
+ * would have asked for them).  Spread over nThreads host threads (<= 0: up
+ * to 16) by slot rows, so no two threads touch one row.  rowResult
+ * (optional) receives each row's store_row result (1 all success / 0).
+ * Returns 0, or < 0 on error. */
+int shd_rowstore_store_rows(ShdRowStore* st, const int32_t* srcs, int32_t count,
+                            const double* lat, const double* rel, const uint8_t* flags,
+                            int64_t ld, int32_t isComplete, const uint8_t* adjacent,
+                            int32_t nThreads, int32_t* rowResult);
 /* topology_incrementPathPacketCounter on a cached entry: 0, or -1 if absent. */
 int shd_rowstore_increment(ShdRowStore* st, int32_t s, int32_t d);
 int64_t shd_rowstore_size(const ShdRowStore* st);

@@ -73,6 +73,8 @@ def _load():
                "orc_topology_cache_size"):
         getattr(lib, fn).argtypes = [vp]
         getattr(lib, fn).restype = C.c_int64
+    lib.orc_bellman_rows.argtypes = [vp, vp, C.c_int32, C.c_int32, vp]
+    lib.orc_bellman_rows.restype = C.c_int32
     lib.orc_selftest_vector_order.argtypes = [C.c_int64, C.c_int32, C.c_uint64]
     lib.orc_selftest_vector_order.restype = C.c_int32
     return lib
@@ -150,6 +152,24 @@ class OracleGraph:
         if rc:
             raise ValueError("orc_rows_parallel failed")
         return dict(lat=lat, rel=rel, hops=hops, pred=pred, flags=flags)
+
+    def bellman_violations(self, sources, lat_rows, targets, threads: int = 1):
+        """Checker: per row, arcs (u, v) whose relaxation would still shorten
+        the row (0 for a shortest-path row).  lat_rows[r][j] = row r's latency
+        to targets[j], which must cover every vertex; the source's own entry
+        (the self-loop path) is replaced by 0."""
+        t = np.asarray(targets)
+        if np.unique(t).shape[0] != self.n or t.shape[0] != self.n:
+            raise ValueError("bellman_violations needs rows over all vertices")
+        R = len(sources)
+        dT = np.empty((self.n, R))
+        dT[t, :] = np.asarray(lat_rows, dtype=np.float64).T
+        dT[np.asarray(sources), np.arange(R)] = 0.0
+        dT = np.ascontiguousarray(dT)
+        viol = np.zeros(R, np.int64)
+        if lib().orc_bellman_rows(self.h, _p(dT), R, int(threads), _p(viol)):
+            raise ValueError("orc_bellman_rows failed")
+        return viol
 
     def direct(self, s, t):
         lat, rel = C.c_double(), C.c_double()

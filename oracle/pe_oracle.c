@@ -546,6 +546,57 @@ int32_t orc_rows_parallel(const OrcGraph* g, const int32_t* sources, int32_t nSo
     return 0;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Checker (not a restatement): the Bellman condition of R rows at once.     */
+/* dT[v * R + r] = row r's distance to vertex v (its source at 0, +inf for   */
+/* unreached); viol[r] counts arcs (u, v) with dT[u] + w < dT[v] (the row is */
+/* then not a shortest-path row).  Threads split the edge list; each edge is */
+/* read once for all R rows.                                                  */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const OrcGraph* g; const double* dT; int32_t R;
+    int64_t e0, e1; int64_t* viol;
+} OrcBell;
+
+static void* bell_worker(void* arg) {
+    OrcBell* b = arg;
+    const OrcGraph* g = b->g;
+    const int32_t R = b->R;
+    for (int64_t e = b->e0; e < b->e1; e++) {
+        const int32_t u = g->from[e], v = g->to[e];
+        if (u == v) continue;
+        const double w = g->lat[e];
+        const double* du = b->dT + (size_t)u * (size_t)R;
+        const double* dv = b->dT + (size_t)v * (size_t)R;
+        for (int32_t r = 0; r < R; r++) {
+            b->viol[r] += (du[r] + w < dv[r]);
+            if (!g->directed) b->viol[r] += (dv[r] + w < du[r]);
+        }
+    }
+    return NULL;
+}
+
+int32_t orc_bellman_rows(const OrcGraph* g, const double* dT, int32_t R, int32_t nThreads,
+                         int64_t* viol) {
+    if (!g || !dT || R < 1 || nThreads < 1 || !viol) return -1;
+    OrcBell* bs = calloc((size_t)nThreads, sizeof(OrcBell));
+    int64_t* cnt = calloc((size_t)nThreads * (size_t)R, sizeof(int64_t));
+    pthread_t* th = malloc(sizeof(pthread_t) * (size_t)nThreads);
+    if (!bs || !cnt || !th) { free(bs); free(cnt); free(th); return -1; }
+    for (int32_t t = 0; t < nThreads; t++) {
+        bs[t] = (OrcBell){g, dT, R, g->m * t / nThreads, g->m * (t + 1) / nThreads,
+                          cnt + (size_t)t * (size_t)R};
+        pthread_create(&th[t], NULL, bell_worker, &bs[t]);
+    }
+    for (int32_t t = 0; t < nThreads; t++) pthread_join(th[t], NULL);
+    for (int32_t r = 0; r < R; r++) {
+        viol[r] = 0;
+        for (int32_t t = 0; t < nThreads; t++) viol[r] += cnt[(size_t)t * (size_t)R + r];
+    }
+    free(bs); free(cnt); free(th);
+    return 0;
+}
+
 /* _topology_lookupDirectPath (topology.c:1877-1927) */
 int32_t orc_direct_path(const OrcGraph* g, int32_t s, int32_t t, double* lat, double* rel) {
     double totalLatency = 0.0, totalReliability = 1.0, ploss;

@@ -99,6 +99,12 @@ int32_t orc_rows_parallel(const OrcGraph* g, const int32_t* sources,
                           double* lat, double* rel, int32_t* hops,
                           int32_t* pred, uint8_t* flags);
 
+/* Checker: Bellman condition for R distance rows at once.  dT is [n][R]
+ * (vertex-major: dT[v*R + r] = row r's distance to v, source 0, +inf
+ * unreached); viol[r] = arcs (u,v) with dT[u] + w < dT[v].  0 / -1. */
+int32_t orc_bellman_rows(const OrcGraph* g, const double* dT, int32_t R, int32_t nThreads,
+                         int64_t* viol);
+
 /* --------------------------------------------------------------------------
  * Path-cache / dispatcher restatement (topology.c:1284-1386, 1969-2092).
  * Queries are by vertex index (the Address->vertex map of topology.c:1388

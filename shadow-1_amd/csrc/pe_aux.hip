@@ -148,9 +148,12 @@ __global__ __launch_bounds__(256) void k_incident_min(DevGraph g0, int32_t* out)
 // One thread: the igraph path of a row whose per-vertex chosen IN-arcs are in
 // P (k_exact_rows' slot after a full emulation), walked from t back to s;
 // out[0] = t ... out[len-1] = s in the CALLER's vertex ids.  *len = -1 when a
-// vertex on the way has no parent (unreached), -2 when the path exceeds cap.
+// vertex on the way has no parent (unreached) or a parent arc outside the
+// graph (stale scratch: the caller checks reachability first), -2 when the
+// path exceeds cap.
 __global__ void k_path_walk(DevGraph g0, const int32_t* __restrict__ P, int s, int t,
-                            int32_t* __restrict__ out, int cap, int32_t* __restrict__ len) {
+                            int32_t* __restrict__ out, int cap, int32_t* __restrict__ len,
+                            int32_t nInArcs) {
     const DevGraph g = global_view(g0);
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int k = 0, v = t;
@@ -160,16 +163,17 @@ __global__ void k_path_walk(DevGraph g0, const int32_t* __restrict__ P, int s, i
         out[k++] = g.oldId ? g.oldId[v] : v;
         if (v == s) break;
         const int a = P[v];
-        if (a < 0) { *len = -1; return; }
+        if (a < 0 || (a & ~TIE_AMB) >= nInArcs) { *len = -1; return; }
         v = g.inCol[a & ~TIE_AMB];
+        if (v < 0 || v >= g.n) { *len = -1; return; }
     }
     *len = k;
 }
 
 void launch_path_walk(const DevGraph& g, const int32_t* dP, int32_t s, int32_t t, int32_t* dOut,
-                      int32_t cap, int32_t* dLen, void* stream) {
+                      int32_t cap, int32_t* dLen, int32_t nInArcs, void* stream) {
     hipLaunchKernelGGL(k_path_walk, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), g, dP, s,
-                       t, dOut, cap, dLen);
+                       t, dOut, cap, dLen, nInArcs);
 }
 
 void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, int64_t nEdges,

@@ -59,11 +59,7 @@ constexpr int WALK_BUDGET = 2048;   // walk steps per target before the deep-tre
 // correcting re-relaxations but saves whole vertex visits (each visit reads
 // one [v][LB] line per arc): C4 schedule simulation (tools/sim) 2.21 -> 1.56
 // arc visits per batch, x m_arcs, at a quarter of the bucket width.
-#ifdef SHDPE_X_LANE_POLICY
-constexpr bool EAGER = false;
-#else
 constexpr bool EAGER = true;
-#endif
 
 struct alignas(16) BCtrl {
     int qtail;
@@ -89,37 +85,19 @@ __device__ __forceinline__ unsigned long long enc_dirty(unsigned long long bits)
 __device__ __forceinline__ unsigned long long dec(unsigned long long e) { return e >> 1; }
 constexpr unsigned long long INF_ENC = (INF_BITS << 1) | 1ull;
 
-// (A/B experiment knobs, see tools/build_variant.sh)
+// (perturbation variants of these three -- plain stores, doubled atomics,
+// doubled reads -- are patches under tools/variants/, built by
+// tools/build_variant.sh for same-box A/B runs)
 __device__ __forceinline__ void relax_min(unsigned long long* p, unsigned long long v) {
-#ifdef SHDPE_X_PLAIN_RELAX
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
     __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef SHDPE_X_DOUBLE_ATOMIC
-    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-#endif
 }
 
-// relax pre-check load (A/B knob: SHDPE_X_DOUBLE_READ also reads the line of
-// the vertex 96 ids lower, same lane: the cost of one more random line read
-// per arc visit)
+// relax pre-check load
 __device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, int x, int LB, int l) {
-#ifdef SHDPE_X_DOUBLE_READ
-    const unsigned long long a = ld_wg(&D[(size_t)x * LB + l]);
-    const int y = x >= 96 ? x - 96 : x;
-    const unsigned long long b = ld_wg(&D[(size_t)y * LB + l]);
-    return b == 12345ull ? b : a;
-#else
     return ld_wg(&D[(size_t)x * LB + l]);
-#endif
 }
 
 __device__ __forceinline__ void mark_clean(unsigned long long* p, unsigned long long e) {
-#ifdef SHDPE_X_PLAIN_CLEAN
-    __hip_atomic_store(p, e | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return;
-#endif
     unsigned long long expect = e;
     (void)__hip_atomic_compare_exchange_strong(p, &expect, e | 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1139,6 +1117,7 @@ int64_t batch_bits_words(int n) { return 2 * (int64_t)((((n + 31) >> 5) + 3) & ~
 template <int WPE, int PART>
 static const void* kptr(int lb, bool gb) {
     if (gb) return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, true, PART>);
+    if (lb == 4) return reinterpret_cast<const void*>(&k_batch_rows<4, WPE, false, PART>);
     if (lb == 8) return reinterpret_cast<const void*>(&k_batch_rows<8, WPE, false, PART>);
     if (lb == 32) return reinterpret_cast<const void*>(&k_batch_rows<32, WPE, false, PART>);
     return reinterpret_cast<const void*>(&k_batch_rows<16, WPE, false, PART>);
@@ -1160,6 +1139,8 @@ static void launch_w(const DevGraph& g, const DevTable& tab, const BatchScratch&
                      const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid) {
     if (cfg.gbits)    // graphs whose bitmaps exceed LDS: LB 16 only (the engine forces it)
         launch_lb<16, WPE, true, PART>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    else if (cfg.lb == 4)
+        launch_lb<4, WPE, false, PART>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (cfg.lb == 8)
         launch_lb<8, WPE, false, PART>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (cfg.lb == 32)

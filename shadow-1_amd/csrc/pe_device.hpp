@@ -200,7 +200,7 @@ int sparse_max_threads();
 // the descriptor; null disables the export).
 // igraph path of one row from k_exact_rows' per-vertex IN-arcs (pe_aux.hip)
 void launch_path_walk(const DevGraph& g, const int32_t* dP, int32_t s, int32_t t, int32_t* dOut,
-                      int32_t cap, int32_t* dLen, void* stream);
+                      int32_t cap, int32_t* dLen, int32_t nInArcs, void* stream);
 void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream,

@@ -76,6 +76,7 @@ struct Shard {
     BatchScratch bsc{};
     bool batchReady = false;
     int32_t batchRound = 0;         // split kernels: batches per round (persisted dist arrays)
+    int32_t batchSlots = 0;         // scratch slots allocated (no launch may exceed it)
     int32_t* dBatchRows = nullptr;
     uint8_t* dBatchAmb = nullptr;
     TieBuf tie{};                   // early-stop tie rows (batched path)
@@ -276,11 +277,15 @@ static int configure(ShdPe* pe, Shard* sh) {
     pe->batched = pe->mode == 1 &&
                   (tu.batch == 1 || (tu.batch != 0 && layout == 0) || pe->opt.forceMode == 5);
     BatchLaunch b{};
-    // LB = 16 sources per batch; 8 when a shard has too few rows to give
-    // every CU a batch of 16 (8-GPU shards of C4)
+    // LB = 16 sources per batch, fewer when a shard has too few rows to give
+    // every resident workgroup (two per CU) a batch: the largest LB of 16 / 8
+    // / 4 with at least 2 x CUs batches (C4: 16 at 1-2 GPUs, 8 at 4, 4 at 8)
     b.lb = tu.batchLB;
-    if (b.lb != 8 && b.lb != 16 && b.lb != 32)
-        b.lb = ((int64_t)sh->rowCount + 15) / 16 < (int64_t)sh->numCUs ? 8 : 16;
+    if (b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32) {
+        const int64_t want = 2 * (int64_t)sh->numCUs;
+        b.lb = ((int64_t)sh->rowCount + 15) / 16 >= want ? 16
+             : ((int64_t)sh->rowCount + 7) / 8 >= want ? 8 : 4;
+    }
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
@@ -836,6 +841,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
         roundB = std::max<size_t>(slots, std::min<size_t>(nBatchesAll, dBudget / perD));
     }
     sh->batchRound = (int32_t)roundB;
+    sh->batchSlots = (int32_t)slots;
     void *D, *R, *H, *P, *q, *rows, *amb, *fl;
     if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
@@ -1065,14 +1071,19 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             if (sh->tie.cap > 0) HIPCHK(hipMemsetAsync(sh->tie.count, 0, 4, sh->stream));
             HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
+            // a workgroup indexes its scratch slot by blockIdx: never launch
+            // more workgroups than ensure_batch allocated slots for
+            BatchLaunch relax = sh->bcfg;
+            relax.grid = std::min(relax.grid, sh->batchSlots);
             if (!sh->bcfg.split) {
-                launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, sh->bcfg,
+                launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows, nB, sh->dBatchAmb, relax,
                                   sh->dDbg, sh->dTie, sh->stream, 0);
             } else {
                 // rounds of batches: relax all of them, then the post kernel
                 // over the same batches (their dist arrays persist in HBM)
                 // (the post kernel may run another variant: bcfgPost)
-                const BatchLaunch& post = sh->bcfgPost.grid > 0 ? sh->bcfgPost : sh->bcfg;
+                BatchLaunch post = sh->bcfgPost.grid > 0 ? sh->bcfgPost : sh->bcfg;
+                post.grid = std::min(post.grid, sh->batchSlots);
                 for (int32_t r0 = 0; r0 < nB; r0 += sh->batchRound) {
                     const int32_t rn = std::min(sh->batchRound, nB - r0);
                     const size_t ro = (size_t)r0 * LB;
@@ -1080,7 +1091,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                     for (int part = 1; part <= 2; ++part) {
                         HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
                         launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows + ro, rn,
-                                          sh->dBatchAmb + ro, part == 1 ? sh->bcfg : post,
+                                          sh->dBatchAmb + ro, part == 1 ? relax : post,
                                           sh->dDbg ? sh->dDbg + 16 * r0 : nullptr, sh->dTie, sh->stream, part);
                         if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[part], sh->stream));
                     }
@@ -1276,6 +1287,12 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
     for (auto& sp : pe->shards) {
         Shard* sh = sp.get();
         if (sh->tuned || (sh->bcfgAlt.grid <= 0 && sh->bcfgAlt2.grid <= 0) || sh->rowCount <= 0) continue;
+        // scratch first: ensure_batch sizes the slots and lowers the live
+        // grids to them, and the candidates below are copies of those grids
+        if (hipSetDevice(sh->device) != hipSuccess) return SHD_PE_EHIP;
+        int rc0 = ensure_table(pe, sh);
+        if (!rc0) rc0 = ensure_batch(pe, sh);
+        if (rc0) return rc0;
         std::vector<int32_t> pos(sh->rowCount);
         for (int32_t i = 0; i < sh->rowCount; ++i) pos[i] = sh->rowStart + i;
         const ShdPeStats keep = sh->stats;
@@ -1577,11 +1594,21 @@ extern "C" int shd_pe_get_path(ShdPe* pe, int32_t srcVertex, int32_t dstVertex, 
         sh->pathSrc = srcVertex;
     }
     int32_t* dLen = sh->dPath + g.n + 32;
+    // reachability from the row the emulation just wrote: an unreached
+    // target has no parent chain in slot 0 (its P entry is whatever an
+    // earlier row left there), so it must not be walked
+    {
+        uint8_t f = 0;
+        const size_t cell = (size_t)(ps - sh->tab.rowStart) * pe->attached.size() + pe->posOf[dstVertex];
+        HIPCHK(hipMemcpyAsync(&f, sh->tab.flags + cell, 1, hipMemcpyDeviceToHost, sh->stream));
+        HIPCHK(hipStreamSynchronize(sh->stream));
+        if (f & F_UNREACHABLE) return SHD_PE_EUNREACHABLE;
+    }
     // device ids of s and t (the batched path relabels vertices)
     int32_t sD = srcVertex, tD = dstVertex;
     if (!pe->devOf.empty()) { sD = pe->devOf[srcVertex]; tD = pe->devOf[dstVertex]; }
     launch_path_walk(sh->dg, sh->sc.pred, sD, tD, sh->dPath, std::min<int32_t>(cap, g.n + 1), dLen,
-                     sh->stream);
+                     (int32_t)g.nArcs(), sh->stream);
     HIPCHK(hipGetLastError());
     int32_t n = 0;
     HIPCHK(hipMemcpyAsync(&n, dLen, 4, hipMemcpyDeviceToHost, sh->stream));

@@ -40,7 +40,7 @@ EXPORTS = [
     "shd_rowstore_get", "shd_rowstore_store", "shd_rowstore_store_row", "shd_rowstore_increment",
     "shd_rowstore_size", "shd_rowstore_min_latency", "shd_rowstore_memory_bytes",
     "shd_pe_host_alloc", "shd_pe_host_free", "shd_pe_tune", "shd_pe_get_path",
-    "shd_rowstore_foreach",
+    "shd_rowstore_foreach", "shd_rowstore_store_rows",
 ]
 
 
@@ -153,6 +153,7 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_tune": (C.c_int, [vp]),
         "shd_pe_get_path": (C.c_int, [vp, i32, i32, vp, i32, vp]),
         "shd_rowstore_foreach": (i64, [vp, vp, vp]),
+        "shd_rowstore_store_rows": (C.c_int, [vp, vp, i32, vp, vp, vp, i64, i32, vp, i32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -325,6 +326,21 @@ class Engine:
         `out` (e.g. from pinned_rows) receives them in place."""
         T = self.T
         if out is not None:
+            # the C side writes count * T elements per field: check every
+            # buffer before handing it over (a short or mistyped one would be
+            # overrun)
+            want = {"lat": np.float64, "rel": np.float64, "hops": np.int32, "flags": np.uint8,
+                    "pred": np.int32}
+            for k, dt in want.items():
+                a = out.get(k)
+                if a is None:
+                    continue
+                if a.dtype != dt or a.ndim != 2 or a.shape[1] != T or a.shape[0] < count \
+                        or not a.flags.c_contiguous:
+                    raise ValueError(f"get_rows: out[{k!r}] must be C-contiguous {np.dtype(dt)} "
+                                     f"of shape (>= {count}, {T}), got {a.dtype} {a.shape}")
+            if out.get("pred") is not None and not self.store_pred:
+                raise ValueError("get_rows: pred requested but the engine stores no predecessors")
             lat, rel, hops, flags, pred = (out[k][:count] if out.get(k) is not None else None
                                            for k in ("lat", "rel", "hops", "flags", "pred"))
         else:
@@ -335,15 +351,16 @@ class Engine:
                                             _p(hops), _p(pred), _p(flags)), "shd_pe_get_rows")
         return dict(lat=lat, rel=rel, hops=hops, pred=pred, flags=flags)
 
-    def pinned_rows(self, count: int) -> dict:
+    def pinned_rows(self, count: int, fields=("lat", "rel", "hops", "flags", "pred")) -> dict:
         """Row buffers for get_rows(out=...) in page-locked host memory
         (shd_pe_host_alloc): the DMA lands in them without a staging copy.
-        Freed when the returned arrays are garbage collected."""
+        Fields not listed are None (not copied).  Freed when the returned
+        arrays are garbage collected."""
         T = self.T
         out = {}
         for k, dt in (("lat", np.float64), ("rel", np.float64), ("hops", np.int32),
                       ("flags", np.uint8), ("pred", np.int32)):
-            if k == "pred" and not self.store_pred:
+            if k not in fields or (k == "pred" and not self.store_pred):
                 out[k] = None
                 continue
             out[k] = _pinned_array((count, T), dt, self._lib)
@@ -491,6 +508,34 @@ class RowStore:
         if rc < 0:
             raise EngineError(rc, "shd_rowstore_store_row")
         return rc == 1
+
+    def store_rows(self, srcs, lat, rel, flags, is_complete=False, adjacent=None,
+                   threads: int = 0) -> np.ndarray:
+        """shd_rowstore_store_rows: rows i = 0..count-1 of (count, >= T) arrays
+        (e.g. Engine.pinned_rows blocks), as store_row on srcs in order; returns
+        each row's all-success flag."""
+        s = np.ascontiguousarray(srcs, dtype=np.int32)
+        count, T = s.shape[0], self._att.shape[0]
+        arrs = {"lat": (lat, np.float64), "rel": (rel, np.float64), "flags": (flags, np.uint8),
+                "adjacent": (adjacent, np.uint8)}
+        ld = None
+        for name, (arr, dt) in arrs.items():
+            if arr is None:
+                continue
+            if arr.dtype != dt or arr.ndim != 2 or not arr.flags.c_contiguous:
+                raise ValueError(f"store_rows: {name} must be a C-contiguous 2-D {np.dtype(dt)} array")
+            if arr.shape[0] < count or arr.shape[1] < T:
+                raise ValueError(f"store_rows: {name} is {arr.shape}, need >= ({count}, {T})")
+            if ld is not None and arr.shape[1] != ld:
+                raise ValueError("store_rows: arrays differ in row length")
+            ld = arr.shape[1]
+        res = np.empty(count, np.int32)
+        rc = self._lib.shd_rowstore_store_rows(self.h, _p(s), count, _p(lat), _p(rel), _p(flags),
+                                               int(ld or T), int(is_complete), _p(adjacent),
+                                               int(threads), _p(res))
+        if rc < 0:
+            raise EngineError(rc, "shd_rowstore_store_rows")
+        return res
 
     def increment(self, s, d) -> int:
         return self._lib.shd_rowstore_increment(self.h, int(s), int(d))

@@ -119,24 +119,30 @@ def _triu_pairs(n: int):
     return iu, ju.astype(np.int32)
 
 
-def dense(n: int = 20_000, seed: int = 3, drop_edge: bool = False) -> Topology:
+def dense(n: int = 20_000, seed: int = 3, drop_edge: bool = False, quantum: float = 0.0) -> Topology:
     """Complete graph + self-loops; ``drop_edge`` removes
-    one non-loop edge so ``_topology_isComplete`` is FALSE (C3b)."""
+    one non-loop edge so ``_topology_isComplete`` is FALSE (C3b); ``quantum``
+    rounds latencies to its multiples (0.005 ms: the tie-stress variant)."""
     rng = np.random.default_rng(seed)
     iu, ju = _triu_pairs(n)
     lat = np.clip(rng.lognormal(np.log(60.0), 0.8, size=iu.shape[0]), 1.0, 2000.0)
+    if quantum > 0:
+        lat = np.maximum(np.round(lat / quantum), 1.0) * quantum
     if drop_edge:
         k = int(rng.integers(iu.shape[0]))
         keep = np.ones(iu.shape[0], dtype=bool)
         keep[k] = False
         iu, ju, lat = iu[keep], ju[keep], lat[keep]
     self_lat = np.clip(rng.lognormal(np.log(60.0), 0.8, size=n), 1.0, 2000.0)
+    if quantum > 0:
+        self_lat = np.maximum(np.round(self_lat / quantum), 1.0) * quantum
     src = np.concatenate([iu, np.arange(n)])
     dst = np.concatenate([ju, np.arange(n)])
     latency = np.concatenate([lat, self_lat])
     return Topology(n=n, directed=False, src=src, dst=dst, latency=latency,
                     loss=np.full(latency.shape[0], 0.005), vloss=np.zeros(n),
-                    name=f"dense{n}_s{seed}" + ("_minus1" if drop_edge else ""))
+                    name=f"dense{n}_s{seed}" + ("_minus1" if drop_edge else "") +
+                    (f"_q{quantum}" if quantum > 0 else ""))
 
 
 def random_sparse(n: int, avg_deg: float, seed: int, directed: bool = False,
@@ -207,6 +213,7 @@ CONFIGS = {
     "c2q": dict(desc="C2 with latencies rounded to 0.005 ms (tie stress, SURVEY.md 8d)"),
     "c3a": dict(desc="dense n=20k complete (configs[2], direct rows)"),
     "c3b": dict(desc="dense n=20k minus one edge (configs[2], min-plus)"),
+    "c3bq": dict(desc="C3b with latencies rounded to 0.005 ms (dense tie stress, SURVEY.md 8d)"),
     "c5": dict(desc="BA n=250k m=2, 65,536 attached (configs[4])"),
     "c5q": dict(desc="C5 with latencies rounded to 0.005 ms (tie stress, SURVEY.md 8d)"),
 }
@@ -219,6 +226,7 @@ def make_config(name: str):
     c1m  shipped topology minus one edge (Dijkstra semantics, tie stress)
     c2   RGG 10k, all sources        c2q  same, latencies rounded to 0.005
     c3a  dense 20k complete           c3b  dense 20k minus one edge
+    c3bq c3b, latencies rounded to 0.005 (SHDPE_C3_N overrides n for all three)
     c4   BA 100k, 16,384 attached     c4q  same, latencies rounded to 0.005
     c5   BA 250k, 65,536 attached     c5q  same, latencies rounded to 0.005
     """
@@ -231,9 +239,9 @@ def make_config(name: str):
         if name == "c1m":
             top = minus_one_edge(top, seed=3)
         return top, np.arange(top.n, dtype=np.int32)
-    if name in ("c3a", "c3b"):
+    if name in ("c3a", "c3b", "c3bq"):
         n = int(__import__("os").environ.get("SHDPE_C3_N", "20000"))
-        top = dense(n, seed=3, drop_edge=(name == "c3b"))
+        top = dense(n, seed=3, drop_edge=(name != "c3a"), quantum=0.005 if name == "c3bq" else 0.0)
         return top, np.arange(top.n, dtype=np.int32)
     if name == "c2":
         top = rgg(10_000, seed=1)

@@ -1,5 +1,6 @@
 // ThreadSanitizer driver for pe_rowstore.cpp: 8 readers (get + increment)
-// race one writer (store_row) on the same store.  Built and run by
+// race one writer (store_row for the first half of the rows, then one
+// 4-thread store_rows bulk fill for the rest) on the same store.  Built and run by
 // tests/test_rowstore.py::test_rowstore_under_thread_sanitizer (host code
 // only, no device).
 #include <atomic>
@@ -34,10 +35,25 @@ int main() {
         });
     std::vector<double> lat(k), rel(k, 0.5);
     std::vector<uint8_t> fl(k, 0);
-    for (int a = 0; a < k; ++a) {
+    const int half = k / 2;
+    for (int a = 0; a < half; ++a) {
         for (int b = 0; b < k; ++b) lat[b] = a <= b ? 1000.0 * a + b : 1000.0 * b + a;
         if (shd_rowstore_store_row(st, att[a], lat.data(), rel.data(), fl.data(), 0, nullptr) < 0)
             return 3;
+    }
+    {
+        const int cnt = k - half;
+        std::vector<int32_t> src(cnt);
+        std::vector<double> L((size_t)cnt * k), R((size_t)cnt * k, 0.5);
+        std::vector<uint8_t> F((size_t)cnt * k, 0);
+        for (int i = 0; i < cnt; ++i) {
+            const int a = half + i;
+            src[i] = att[a];
+            for (int b = 0; b < k; ++b) L[(size_t)i * k + b] = a <= b ? 1000.0 * a + b : 1000.0 * b + a;
+        }
+        if (shd_rowstore_store_rows(st, src.data(), cnt, L.data(), R.data(), F.data(), k, 0, nullptr, 4,
+                                    nullptr) < 0)
+            return 5;
     }
     stop = true;
     for (auto& t : th) t.join();

@@ -556,6 +556,48 @@ def test_batched_kernel_each_variant(E, oracle_mod, monkeypatch, wpe, case):
         assert st["rowsExact"] > 0
 
 
+@pytest.mark.parametrize("lb", [4, 8, 16])
+@pytest.mark.parametrize("wpe", [4, 8])
+@pytest.mark.parametrize("case", ["power_law", "quantized"])
+def test_batched_kernel_each_lb(E, oracle_mod, monkeypatch, lb, wpe, case):
+    """Every batch width the engine may pick by shard size (LB 16 / 8 / 4
+    sources per batch: 8-GPU shards of C4 take LB 4), forced through
+    SHDPE_BATCH_LB at both register budgets, bit-exact with the oracle, tie
+    rows and a ragged last batch included."""
+    monkeypatch.setenv("SHDPE_BATCH_LB", str(lb))
+    monkeypatch.setenv("SHDPE_BATCH_WPE", str(wpe))
+    if case == "power_law":
+        top = G.power_law(8000, m=3, seed=15)
+        att = G.sample_attached(top.n, 1203, seed=4)
+        srcs = att[::3]
+    else:
+        top, att, srcs = G.random_sparse(600, 6, seed=215, quantum=1.0), np.arange(599), None
+    st = _check_engine(E, oracle_mod, top, att, sources=srcs, force=5, debug_flags=E.DEBUG_ENV)
+    assert st["batched"] == 1 and st["batchLanes"] == lb and st["batchWaves"] == wpe
+    if case == "quantized":
+        assert st["rowsExact"] > 0
+
+
+def test_tune_with_fewer_scratch_slots_than_grid(E, oracle_mod, monkeypatch):
+    """A scratch budget below the resident grid (huge graphs, or a small
+    SHDPE_BATCH_SCRATCH_GB): shd_pe_tune must time its variants -- and keep
+    one -- with grids no larger than the slots allocated (a workgroup indexes
+    its slot by blockIdx); rows stay bit-exact."""
+    monkeypatch.setenv("SHDPE_BATCH_SCRATCH_GB", "0.3")     # ~25 slots of a 30k-vertex graph
+    top = G.power_law(30_000, 3, seed=6)
+    att = np.arange(0, top.n, 11, dtype=np.int32)
+    eng = E.Engine(top, att, force_mode=5, debug_flags=E.DEBUG_ENV)
+    eng.tune()
+    eng.compute_all()
+    og = oracle_mod.OracleGraph(top)
+    pos = np.arange(0, eng.T, 61)
+    exp = og.rows(eng.attached[pos], eng.attached, threads=8)
+    for i, p in enumerate(pos):
+        got = {k: (v[0] if v is not None else None) for k, v in eng.get_rows(int(p), 1).items()}
+        _assert_rows_equal(got, {k: v[i] for k, v in exp.items()}, f"row {p}")
+    eng.close()
+
+
 def _oracle_path(top, og, s, t, att):
     """igraph's path s -> t from the oracle's raw Dijkstra (parent edge ids)."""
     _, par, _ = og.raw(int(s), att)
@@ -606,6 +648,28 @@ def test_get_path_matches_igraph(E, oracle_mod, case):
         eng.get_path(s0, t0, cap=1)
     with pytest.raises(E.EngineError):
         eng.get_path(s0, 1)               # vertex 1 is not attached
+    eng.close()
+
+
+@pytest.mark.parametrize("force_mode", [0, 5])
+def test_get_path_unreachable_is_eunreachable(E, force_mode):
+    """Two disjoint components: a target in the other one has no parent chain.
+    shd_pe_get_path must say SHD_PE_EUNREACHABLE (from the row's flags), never
+    walk the stale scratch parents left there by an earlier row."""
+    a, b = G.random_sparse(300, 4, seed=41), G.random_sparse(200, 4, seed=42)
+    top = Topology(n=500, directed=False, src=np.concatenate([a.src, b.src + 300]),
+                   dst=np.concatenate([a.dst, b.dst + 300]),
+                   latency=np.concatenate([a.latency, b.latency]),
+                   loss=np.concatenate([a.loss, b.loss]))
+    att = np.arange(0, 500, 5, dtype=np.int32)
+    eng = E.Engine(top, att, force_mode=force_mode)
+    eng.compute_all()
+    for s, t in ((0, 305), (310, 5), (5, 400), (450, 10)):
+        assert eng.get_path(10, 20)[0] == 10           # leaves a full parent array behind
+        with pytest.raises(E.EngineError) as ei:
+            eng.get_path(s, t)
+        assert ei.value.code == E.EUNREACHABLE, (s, t, ei.value)
+    assert eng.get_path(305, 400)[-1] == 400
     eng.close()
 
 

@@ -185,3 +185,48 @@ def test_rowstore_under_thread_sanitizer(tmp_path):
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout, r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_store_rows_equals_sequential_store_row(threads):
+    """shd_rowstore_store_rows (the whole-table fill, threads by slot rows)
+    leaves exactly what store_row over the same sources in the same order
+    does: first stored direction wins, unreachable / failed targets, complete
+    and prefersDirectPaths refusals, per-row isAllSuccess, min latency."""
+    n, k = 500, 97
+    att = _attached(n, k, 11)
+    rng = np.random.default_rng(threads)
+    order = rng.permutation(k)
+    order = np.concatenate([order, order[:10]])         # repeated sources: nothing new
+    srcs = att[order]
+    lat = rng.uniform(1, 100, size=(srcs.shape[0], k + 3))   # ld > T
+    rel = rng.uniform(0.5, 1, size=lat.shape)
+    flags = np.zeros(lat.shape, np.uint8)
+    flags[rng.random(lat.shape) < 0.03] = F_UNREACHABLE
+    flags[rng.random(lat.shape) < 0.01] = F_NOEDGE
+    adj = (rng.random(lat.shape) < 0.05).astype(np.uint8)
+    for is_complete, use_adj in ((False, False), (False, True), (True, False)):
+        a, b = RowStore(n, att), RowStore(n, att)
+        a.store(int(att[5]), int(att[9]), 1, 0, 0, 0.5, 0.25)   # a prior direct entry
+        b.store(int(att[5]), int(att[9]), 1, 0, 0, 0.5, 0.25)
+        A = adj if use_adj else None
+        want = [a.store_row(int(s), lat[i], rel[i], flags[i], is_complete,
+                            None if A is None else A[i]) for i, s in enumerate(srcs)]
+        got = b.store_rows(srcs, lat, rel, flags, is_complete, A, threads=threads)
+        assert [bool(x) for x in got] == want
+        assert a.size() == b.size() and a.min_latency() == b.min_latency()
+        assert sorted(a.items()) == sorted(b.items())
+
+
+def test_store_rows_rejects_bad_buffers():
+    att = np.arange(0, 40, 2, dtype=np.int32)
+    st = RowStore(40, att)
+    lat = np.ones((3, 20)); rel = np.ones((3, 20)); fl = np.zeros((3, 20), np.uint8)
+    with pytest.raises(ValueError):
+        st.store_rows(att[:4], lat, rel, fl)                 # 4 rows, buffers hold 3
+    with pytest.raises(ValueError):
+        st.store_rows(att[:3], lat[:, :10], rel[:, :10], fl[:, :10])   # rows shorter than T
+    with pytest.raises(ValueError):
+        st.store_rows(att[:3], lat.astype(np.float32), rel, fl)
+    with pytest.raises(Exception):
+        st.store_rows(np.array([1, 2, 3], np.int32), lat, rel, fl)    # 1 is not attached
