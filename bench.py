@@ -233,12 +233,19 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries exactly one line, rank 0's JSON: whatever the libraries
+    # print there (gloo's connection notices, RCCL) goes to stderr instead
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    emit = (lambda line: os.write(out_fd, (line + "\n").encode())) if rank == 0 else (lambda line: None)
     if args.dry_launch:
-        sys.stdout.write(json.dumps({"rank": rank, "local_rank": local, "world": world,
-                                     "master": f"{os.environ.get('MASTER_ADDR')}:"
-                                               f"{os.environ.get('MASTER_PORT')}",
-                                     "pid": os.getpid()}) + "\n")   # one write: no interleaving
-        sys.stdout.flush()
+        if os.environ.get("BENCH_DRY_NOISE"):
+            os.write(1, b"[Gloo] Rank is connected to 1 peer ranks\n")   # a library's stdout chatter
+        os.write(out_fd, (json.dumps({"rank": rank, "local_rank": local, "world": world,
+                                      "master": f"{os.environ.get('MASTER_ADDR')}:"
+                                                f"{os.environ.get('MASTER_PORT')}",
+                                      "pid": os.getpid()}) + "\n").encode())   # one write
         # launcher self-test hooks: one rank fails, the others hang
         if os.environ.get("BENCH_DRY_FAIL_RANK") == str(rank):
             sys.exit(3)
@@ -409,8 +416,7 @@ def main():
         out["secondary"] = [secondary(wl, args.steps, dbg) for wl in args.secondary.split(",") if wl]
     if rank == 0 and world == 1 and args.tie_stress:
         out["tie_stress"] = [tie_stress(wl, args.steps, dbg) for wl in args.tie_stress.split(",") if wl]
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    emit(json.dumps(out))
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

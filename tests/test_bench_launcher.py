@@ -51,3 +51,13 @@ def test_failing_rank_stops_the_others():
     assert r.returncode == 3, (r.returncode, r.stderr)
     assert "rank 2 exited with 3" in r.stderr
     assert time.time() - t0 < 60          # the sleeping ranks were terminated
+
+
+def test_library_stdout_chatter_goes_to_stderr():
+    """Only JSON on stdout: a library printing to fd 1 in a rank (gloo does)
+    lands on stderr."""
+    r = _run(["--gpus", "2", "--dry-launch"], {"BENCH_DRY_NOISE": "1"})
+    assert r.returncode == 0
+    out = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(out) == 2 and all(x.startswith("{") for x in out), r.stdout
+    assert "[Gloo]" in r.stderr

@@ -33,6 +33,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     uint64_t* dirty = calloc(n, 8);
     uint8_t* farp = calloc(n, 1);
     int32_t* stamp = malloc(sizeof(int32_t) * n);
+    uint64_t* hpend = calloc(n, 8);   // lanes whose heavy arcs wait for their bucket to settle
     for (int v = 0; v < n; ++v) stamp[v] = -1;
     int32_t gphase = 0;
     if (!D || !pend || !nextp || !q) return -1;
@@ -46,6 +47,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
         memset(pend, 0, n);
         memset(dirty, 0, 8 * (size_t)n);
         memset(farp, 0, n);
+        memset(hpend, 0, 8 * (size_t)n);
         double farMin = INFINITY;
         double maxOff = 0;
         for (int l = 0; l < LB; ++l) {
@@ -69,6 +71,43 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 if (pend[v] && rowPtr[v + 1] - rowPtr[v] >= heavyDeg) q[qn++] = v;
             for (int v = 0; v < n; ++v)
                 if (pend[v] && rowPtr[v + 1] - rowPtr[v] < heavyDeg) q[qn++] = v;
+            if (qn == 0 && (farMode & 4)) {
+                // bucket settled: heavy arcs (w >= delta) of the lanes whose
+                // key is below the bound, once, with their final values
+                for (int u = 0; u < n; ++u) {
+                    if (!hpend[u]) continue;
+                    uint64_t go = 0;
+                    double du[64];
+                    for (int l = 0; l < LB; ++l) {
+                        du[l] = D[(size_t)u * LB + l];
+                        if (((hpend[u] >> l) & 1) && KEY(u, l, du[l]) < bound) go |= 1ull << l;
+                    }
+                    if (!go) continue;
+                    hpend[u] &= ~go;
+                    out->procs += 1;
+                    for (int a = rowPtr[u]; a < rowPtr[u + 1]; ++a) {
+                        const double w = lat[a];
+                        if (w < delta) continue;
+                        const int x = col[a];
+                        out->arcs += 1;
+                        int anyImp = 0;
+                        for (int l = 0; l < LB; ++l) {
+                            if (!((go >> l) & 1)) continue;
+                            const double nb = du[l] + w;
+                            if (nb < D[(size_t)x * LB + l]) {
+                                D[(size_t)x * LB + l] = nb;
+                                const double kx = KEY(x, l, nb);
+                                if (kx < bound) nextp[x] = 1;   // cannot happen (w >= delta)
+                                else { farp[x] = 1; if (kx < farMin) farMin = kx; }
+                                dirty[x] |= 1ull << l;
+                                anyImp = 1;
+                                out->laneImp += 1;
+                            }
+                        }
+                        out->improving += anyImp;
+                    }
+                }
+            }
             if (qn == 0) {
                 if (!farMode || farMin == INFINITY) break;
                 const double mn = farMin;
@@ -119,10 +158,12 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 dirty[u] &= ~act;
                 out->procs += 1;
                 out->lanesAct += __builtin_popcountll(act);
-                out->arcs += rowPtr[u + 1] - rowPtr[u];
+                if (farMode & 4) hpend[u] |= act;
                 for (int a = rowPtr[u]; a < rowPtr[u + 1]; ++a) {
                     const int x = col[a];
                     const double w = lat[a];
+                    if ((farMode & 4) && w >= delta) continue;
+                    out->arcs += 1;
                     if (stamp[x] != gphase) { stamp[x] = gphase; out->touched += 1; }
                     int anyImp = 0;
                     for (int l = 0; l < LB; ++l) {
@@ -162,5 +203,6 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     free(dirty);
     free(farp);
     free(stamp);
+    free(hpend);
     return 0;
 }
