@@ -182,6 +182,13 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
                        bool forceGlobalHeap, const int32_t* dSlots, const TieBuf& tie,
                        long long* dXdbg, void* stream);
 int exact_soa_max_n();
+// tie rows of dense graphs (mode 3): the same emulation with the popped
+// vertex's ~n arcs scanned by a whole 1024-thread workgroup; dList: per grid
+// slot `stride` entries of exact_dense_list_bytes()
+void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc, void* dList,
+                        void* stream);
+int exact_dense_list_bytes();
 // tie rows whose ambiguous entries lie on no target's path: thr := -1 (the
 // exact kernel then keeps the fast-path parents)
 void launch_tie_scan(const DevGraph& g, const int32_t* dRows, const int32_t* dSlots,

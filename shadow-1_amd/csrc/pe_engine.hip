@@ -87,6 +87,7 @@ struct Shard {
     double *dW = nullptr, *dRl = nullptr, *dD = nullptr;
     int32_t* dP = nullptr;
     uint8_t *dRowA = nullptr, *dRowB = nullptr, *dRowAmbD = nullptr, *dChunkEpoch = nullptr;
+    void* dXList = nullptr;         // k_exact_dense: per slot its pushes / modifies of a pop
     int32_t* dAny = nullptr;
     int32_t denseRows = 0;
     DevTable full{};                // whole table on this device after gather
@@ -268,7 +269,8 @@ static int configure(ShdPe* pe, Shard* sh) {
     // tail in the global slot.
     const bool soa = n <= exact_soa_max_n() && tu.exactHc <= 0;
     const long perWG = soa ? 16L * n + 16 : std::min<long>(LDS, 12L * n + 16);
-    sh->exactHc = (int)std::max<long>(1, std::min<long>(n, (std::min<long>(LDS, perWG) - 16) / 12));
+    // (512 B of the LDS stay free for the kernels' static shared variables)
+    sh->exactHc = (int)std::max<long>(1, std::min<long>(n, (std::min<long>(LDS - 512, perWG) - 16) / 12));
     if (tu.exactHc > 0) sh->exactHc = std::min(sh->exactHc, tu.exactHc);   // tests: global heap tail
     const int exPerCU = (int)std::max<long>(1, std::min<long>(8, LDS / perWG));
     sh->exactGrid = sh->numCUs * (tu.exactPerCU > 0 ? tu.exactPerCU : exPerCU);
@@ -277,15 +279,14 @@ static int configure(ShdPe* pe, Shard* sh) {
     pe->batched = pe->mode == 1 &&
                   (tu.batch == 1 || (tu.batch != 0 && layout == 0) || pe->opt.forceMode == 5);
     BatchLaunch b{};
-    // LB = 16 sources per batch, fewer when a shard has too few rows to give
-    // every resident workgroup (two per CU) a batch: the largest LB of 16 / 8
-    // / 4 with at least 2 x CUs batches (C4: 16 at 1-2 GPUs, 8 at 4, 4 at 8)
+    // LB = 16 sources per batch; 8 when a shard has too few rows to give
+    // every resident workgroup (two per CU) a batch of 16.  C4 per-rank shard
+    // times (profiles/r04_shard_times.txt): N=4 (4,096 rows) LB 8 39.0 ms vs
+    // LB 16 42.7; N=8 (2,048 rows) LB 8 23.7 vs LB 16 39.5 vs LB 4 28.3 --
+    // LB 4 (32-B line pieces) stays a SHDPE_BATCH_LB option only
     b.lb = tu.batchLB;
-    if (b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32) {
-        const int64_t want = 2 * (int64_t)sh->numCUs;
-        b.lb = ((int64_t)sh->rowCount + 15) / 16 >= want ? 16
-             : ((int64_t)sh->rowCount + 7) / 8 >= want ? 8 : 4;
-    }
+    if (b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32)
+        b.lb = ((int64_t)sh->rowCount + 15) / 16 >= 2 * (int64_t)sh->numCUs ? 16 : 8;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
@@ -1195,11 +1196,20 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 dSl = sh->dSlots;
                 while (nTie < (int32_t)exactSlots.size() && exactSlots[nTie] >= 0) ++nTie;
             }
+            const bool dense = pe->mode == 3 && pe->opt.forceMode != 3 && !dSl;
+            if (dense && !sh->dXList &&
+                (rc = dev_alloc(sh, &sh->dXList, (size_t)sh->exactGrid * (size_t)sh->sc.stride *
+                                                     (size_t)exact_dense_list_bytes())))
+                return rc;
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             if (nTie > 0) launch_tie_scan(sh->dg, sh->dRows, sh->dSlots, nTie, sh->tie, sh->stream);
-            launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
-                              sh->exactGrid, sh->exactHc, pe->tu.exactHc > 0, dSl, sh->tie,
-                              sh->dXdbg, sh->stream);
+            if (dense)      // ~n arcs per pop: the workgroup-wide scan
+                launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
+                                   sh->exactGrid, sh->exactHc, sh->dXList, sh->stream);
+            else
+                launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
+                                  sh->exactGrid, sh->exactHc, pe->tu.exactHc > 0, dSl, sh->tie,
+                                  sh->dXdbg, sh->stream);
             HIPCHK(hipGetLastError());
             if (nTie > 0) {
                 launch_tie_write(sh->dg, sh->tab, sh->dRows, sh->dSlots, nTie, sh->tie, sh->stream);

@@ -1530,6 +1530,172 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
 }
 
 // ---------------------------------------------------------------------------
+// k_exact_dense: the same igraph 0.7.1 Dijkstra + 2-way heap emulation for
+// tie rows of DENSE graphs (mode 3), one 1024-thread workgroup per row.  A
+// dense vertex has ~n arcs, so a pop is dominated by the arc scan, which one
+// wave (k_exact_rows) walks in dependent 64-arc chunks (~350 us per pop at
+// n = 20k).  Here waves 1..15 scan contiguous segments of the popped
+// vertex's arcs in parallel (coalesced col / lat / index2 / dist loads; the
+// decision for arc k depends only on v_k's own state, as in k_exact_rows)
+// while wave 0 sifts the heap down -- the scan reads only categories and
+// distances, which a sift-down does not change.  Each scanning wave appends
+// its pushes / modifies to a list of its own in incidence order; after a
+// barrier wave 0 applies the lists in segment order, i.e. in igraph's
+// incidence order, with the wave-parallel WHeap operations.  Same heap array,
+// same pop order, same parents as the one-wave kernel.
+// ---------------------------------------------------------------------------
+constexpr int XD_THREADS = 1024;
+constexpr int XD_SCAN_WAVES = XD_THREADS / 64 - 1;
+
+struct alignas(16) XdEntry {
+    double alt;      // new tentative distance
+    int32_t v;       // vertex
+    int32_t st;      // 0: push (never reached), >= 2: modify (index2 at scan time)
+};
+
+__global__ __launch_bounds__(XD_THREADS) void k_exact_dense(DevGraph g0, DevTable tab0,
+                                                            DevScratch sc0,
+                                                            const int32_t* __restrict__ rows,
+                                                            int32_t nRows, int32_t hc,
+                                                            XdEntry* __restrict__ lists) {
+    const DevGraph g = global_view(g0);
+    const DevTable tab = global_view(tab0);
+    const DevScratch sc = global_view(sc0);
+    const int n = g.n;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const size_t slot = (size_t)blockIdx.x * (size_t)sc.stride;
+    double* D = sc.dist + slot;
+    int32_t* H = sc.hops + slot;
+    double* R = sc.rel + slot;
+    int32_t* P = sc.pred + slot;
+    double* tailKey = reinterpret_cast<double*>(sc.heapTail) + (size_t)blockIdx.x * 2 * sc.heapStride;
+    const WHeap h{tailKey, reinterpret_cast<int32_t*>(tailKey + sc.heapStride), sc.index2 + slot, hc};
+    XdEntry* list = as_global(lists) + (size_t)blockIdx.x * (size_t)sc.stride;
+    __shared__ int sU, sDone, sSeg;
+    __shared__ double sMind;
+    __shared__ int sCnt[XD_SCAN_WAVES];
+    const int ldsLevel = 30 - __builtin_clz(hc + 1);
+    for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
+        const int r = rows[b];
+        const int s = g.attached[r];
+        for (int v = tid; v < n; v += XD_THREADS) h.I2[v] = 0;
+        __syncthreads();
+        if (tid == 0) {
+            h.put(0, 0.0, s);
+            D[s] = 0.0;
+            H[s] = 0;
+            R[s] = 1.0;
+            P[s] = -1;
+        }
+        __syncthreads();
+        int toReach = g.T;      // wave 0's
+        int size = 1;           // wave 0's
+        double km = 0.0;
+        int im = 0;
+        for (;;) {
+            // ---- pop (wave 0): the top, the last element --------------------
+            if (wave == 0) {
+                int done = size <= 0 || toReach <= 0;
+                if (!done) {
+                    const int u = __builtin_amdgcn_readfirstlane(h.lidx()[0]);
+                    const double mind = -h.lkey()[0];
+                    size -= 1;
+                    if (size > 0) h.get(size, km, im);
+                    if (lane == 0) {
+                        __hip_atomic_store(&h.I2[u], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        sU = u;
+                        sMind = mind;
+                        sSeg = (g.rowPtr[u + 1] - g.rowPtr[u] + XD_SCAN_WAVES - 1) / XD_SCAN_WAVES;
+                    }
+                    if (g.isAttached[u]) --toReach;
+                }
+                if (lane == 0) sDone = done;
+            }
+            __syncthreads();
+            if (sDone) break;
+            const int u = sU;
+            const double mind = sMind;
+            const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
+            if (wave == 0) {
+                // ---- sink (wave 0) while waves 1.. scan ---------------------
+                if (size > 0) {
+                    int head = 0, hl = 0;
+                    bool placed = false;
+                    while (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+                }
+            } else {
+                // ---- scan: wave w takes arcs [a0 + (w-1) seg, a0 + w seg) -------
+                const int seg = sSeg;
+                const int lo = a0 + (wave - 1) * seg;
+                const int hi = min(a1, lo + seg);
+                const int hu = ld_wg(&H[u]);
+                const double ru = ld_wg(&R[u]);
+                XdEntry* wl = list + (size_t)(wave - 1) * seg;
+                int cnt = 0;
+                for (int base = lo; base < hi; base += 64) {
+                    const int a = base + lane;
+                    const bool valid = a < hi;
+                    int v = 0, st = 1;
+                    double w = 0.0, dv = 0.0;
+                    if (valid) {
+                        v = g.col[a];
+                        w = g.lat[a];
+                        st = ld_wg(&h.I2[v]);
+                        dv = ld_wg(&D[v]);
+                    }
+                    const double alt = mind + w;
+                    const bool need = valid && (st == 0 || (st >= 2 && alt < dv));
+                    if (need) {
+                        __hip_atomic_store(&P[v], g.outToIn[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&D[v], alt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&H[v], hu + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&R[v], ru * g.rel[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    const unsigned long long m = __ballot(need);
+                    if (need) {
+                        const int k = cnt + __popcll(m & ((1ull << lane) - 1));
+                        wl[k] = XdEntry{alt, v, st};
+                    }
+                    cnt += __popcll(m);
+                }
+                if (lane == 0) sCnt[wave - 1] = cnt;
+            }
+            fence_wg();
+            __syncthreads();
+            // ---- pushes / modifies in incidence order (wave 0) --------------
+            if (wave == 0) {
+                const int seg = sSeg;
+                for (int w = 0; w < XD_SCAN_WAVES; ++w) {
+                    const int cnt = sCnt[w];
+                    const XdEntry* wl = list + (size_t)w * seg;
+                    for (int c0 = 0; c0 < cnt; c0 += 64) {
+                        XdEntry e{0.0, 0, 0};
+                        if (c0 + lane < cnt) e = wl[c0 + lane];
+                        const int ce = min(64, cnt - c0);
+                        for (int k = 0; k < ce; ++k) {
+                            const int vk = __builtin_amdgcn_readlane(e.v, k);
+                            const int sk = __builtin_amdgcn_readlane(e.st, k);
+                            const double ak = readlane_f64(e.alt, k);
+                            if (sk == 0) {              // igraph_2wheap_push_with_index
+                                h.shift_up(size, -ak, vk, lane);
+                                size += 1;
+                            } else {                    // igraph_2wheap_modify (sink is a no-op)
+                                const int p2 = __builtin_amdgcn_readfirstlane(h.I2[vk]);
+                                h.shift_up(p2 - 2, -ak, vk, lane);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        write_row(g, tab, r, s, [&](int t) { return ld_wg(&h.I2[t]) == 1 ? d2b(ld_wg(&D[t])) : INF_BITS; },
+                  [&](int t) { return ld_wg(&H[t]); }, R, P, F_EXACT, tid, XD_THREADS);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_direct_rows: complete graphs (and prefersDirectPaths pairs): row entry =
 // _topology_lookupDirectPath (topology.c:1877-1927).
 // ---------------------------------------------------------------------------
@@ -1660,6 +1826,23 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
     hipLaunchKernelGGL(k_exact_rows, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc, dRows,
                        nRows, hc, dSlots, tie, dXdbg);
 }
+
+void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
+                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc, void* dList,
+                        void* stream) {
+    if (nRows <= 0) return;
+    if (grid > nRows) grid = nRows;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // (the engine's hc leaves 512 B of LDS for the static shared variables;
+    // the heap tail slots are sized for exactly that hc)
+    const int bytes = (int)(((size_t)12 * hc + 15) & ~(size_t)15);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_dense),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    hipLaunchKernelGGL(k_exact_dense, dim3(grid), dim3(XD_THREADS), bytes, st, g, tab, sc, dRows, nRows,
+                       hc, reinterpret_cast<XdEntry*>(dList));
+}
+
+int exact_dense_list_bytes() { return (int)sizeof(XdEntry); }
 
 void launch_direct_rows(const DevGraph& g, const DevTable& tab, const int32_t* dRows,
                         int32_t nRows, void* stream) {
