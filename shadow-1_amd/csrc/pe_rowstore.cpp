@@ -351,16 +351,27 @@ extern "C" int shd_rowstore_store_rows(ShdRowStore* st, const int32_t* srcs, int
         }
         return SHD_PE_OK;
     }
-    // slot-row ownership: equal numbers of slots (row a holds T - a)
+    // slot-row ownership, balanced for THIS call's work: row r gets one put
+    // per source p > r (target r, slot p - r) plus the T - r puts of its own
+    // row when r is a source itself
     std::vector<int32_t> rb(nt + 1, T);
     {
-        const double total = 0.5 * (double)T * (double)(T + 1);
-        double cum = 0.0;
+        std::vector<int64_t> w(T + 1, 0);
+        for (int32_t i = 0; i < count; ++i) w[ps[i]] += T - ps[i];   // own row segment
+        std::vector<int32_t> atLeast(T + 1, 0);   // sources with ordinal p, suffix-summed below
+        for (int32_t i = 0; i < count; ++i) atLeast[ps[i]]++;
+        int64_t greater = 0, total = 0;
+        for (int32_t r = T - 1; r >= 0; --r) {     // sources with p > r
+            w[r] += greater;
+            greater += atLeast[r];
+            total += w[r];
+        }
+        int64_t cum = 0;
         int t = 1;
         rb[0] = 0;
-        for (int32_t a = 0; a < T && t < nt; ++a) {
-            cum += (double)(T - a);
-            while (t < nt && cum >= total * t / nt) rb[t++] = a + 1;
+        for (int32_t r = 0; r < T && t < nt; ++r) {
+            cum += w[r];
+            while (t < nt && (double)cum >= (double)total * t / nt) rb[t++] = r + 1;
         }
     }
     struct Acc { int64_t added = 0; double mn = INFINITY; int err = 0; Arena ar; };
