@@ -31,6 +31,11 @@ for st in ${STAGES:-tests bench}; do
       env $e timeout -k 10 400 python3 -u tools/shard_time.py ${SHARD_WL:-c4} ${SHARD_NS:-1 2 4 8} >> $OUT/shard.txt 2>> $OUT/shard.err || { tail -20 $OUT/shard.err; exit 1; }
     done
     cat $OUT/shard.txt ;;
+  sharddbg)
+    # k_batch_rows counters (per-batch cost spread, phases, arc visits) of
+    # rank 0's shard at N = $SHARD_NS
+    SHDPE_DEBUG=1 timeout -k 10 400 python3 -u tools/shard_time.py ${SHARD_WL:-c4} ${SHARD_NS:-8} > $OUT/sharddbg.txt 2> $OUT/sharddbg.err || { tail -20 $OUT/sharddbg.err; exit 1; }
+    cat $OUT/sharddbg.txt; grep "shdpe\] .*batch" $OUT/sharddbg.err | tail -12 ;;
   bench)
     for wl in ${WLS//,/ }; do
       timeout -k 10 300 python3 -u bench.py --workload $wl --steps ${STEPS:-3} --warmup 1 $QUICK > $OUT/bench_$wl.json 2> $OUT/bench_$wl.err || { tail -20 $OUT/bench_$wl.err; exit 1; }
