@@ -72,6 +72,7 @@ struct alignas(16) BCtrl {
     unsigned long long busyMax;
     unsigned long long busySum;
     double maxOff;    // largest lane offset of the batch (bits via atomicMax)
+    int pubCnt;       // cooperative relax: near bits published this phase
 };
 
 // Entry encoding of the [v][LB] distance array: (f64 bits << 1) | clean.
@@ -188,6 +189,34 @@ __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
     return acc;
 }
 
+// Cooperative relax (PART 1, bs.coopK > 1): K workgroups share one batch.
+// Their shared state lives in uncached memory (memory-side coherent across
+// XCDs): the dist array (atomics and loads), each member's published near
+// bitmap and scalars.  group_barrier: every wave drains its memory
+// operations, one lane adds to the group's counter (memory-side atomic) and
+// polls it until all K members arrived for this epoch.  A poll that runs
+// past the spin limit (members not co-resident: never with the engine's
+// occupancy-sized grid) gives up and reports failure instead of hanging.
+__device__ __forceinline__ bool group_barrier(int* bar, int K, int& epoch) {
+    __shared__ int ok;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    ++epoch;
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int target = epoch * K;
+        int good = 1;
+        for (long long spin = 0;; ++spin) {
+            if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            if (spin > (1ll << 24)) { good = 0; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
 // PART 0: the whole batch in one kernel (relax, predecessors over every
 // vertex, labels + writer, tie export).  PART 1 / 2: the same split in two
 // kernels over a round of batches whose dist arrays persist in HBM between
@@ -230,6 +259,20 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const size_t slot = blockIdx.x;
     const size_t NS = (size_t)bs.nStride;
     const size_t SE = NS * LB;
+    // cooperative relax: K members per batch (static batch assignment)
+    const int coopK = PART == 1 ? bs.coopK : 1;
+    const bool coop = coopK > 1;
+    const int member = coop ? (int)(blockIdx.x % coopK) : 0;
+    const int group = coop ? (int)(blockIdx.x / coopK) : 0;
+    const int nGroups = coop ? (int)(gridDim.x / coopK) : 1;
+    uint32_t* pubNear = coop ? bs.pub + (size_t)group * coopK * nwp : nullptr;
+    unsigned long long* pubS = coop ? bs.pubS + (size_t)group * coopK * 2 : nullptr;
+    int* bar = coop ? bs.bar + group * 16 : nullptr;
+    int epoch = 0, citer = 0;
+    // post kernel over sub-batches: 2^subShift items per batch, LB of the
+    // batch's LB << subShift lanes each (dist arrays keep the full stride)
+    const int subShift = PART == 2 ? bs.subShift : 0;
+    const int DLB = LB << subShift;
     unsigned long long* D = as_global(bs.D + slot * SE);
     double* R = as_global(bs.R + slot * SE);
     int32_t* H = as_global(bs.H + slot * SE);
@@ -240,21 +283,25 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     // by ~20%, and a workgroup finishing early takes the next one)
     __shared__ int nextB;
     for (;;) {
-        if (tid == 0) nextB = atomicAdd(bs.next, 1);
+        if (tid == 0) nextB = coop ? group + (citer++) * nGroups : atomicAdd(bs.next, 1);
         __syncthreads();
-        const int b = nextB;
-        if (b >= nBatches) break;
-        const int row = batchRows[(size_t)b * LB + l];
+        const int item = nextB;
+        if (item >= (nBatches << subShift)) break;
+        const int b = item >> subShift;
+        const int dl = ((item & ((1 << subShift) - 1)) * LB) + l;   // lane within the batch
+        const int row = batchRows[(size_t)b * DLB + dl];
         const int src = row >= 0 ? g.attached[row] : -1;
         if (gid == 0) laneRow[l] = row;
-        if constexpr (PART != 0) D = as_global(bs.D + (size_t)b * SE);
+        if constexpr (PART != 0) D = as_global(bs.D + (size_t)b * NS * DLB);
         // ---- init: dist = +inf (clean) for all (v, lane); pending sets empty ----
         {
             ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
             const size_t cnt2 = NE / 2;
             const ulonglong2 inf2 = make_ulonglong2(INF_ENC, INF_ENC);
-            if constexpr (PART != 2)
-                for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
+            if constexpr (PART != 2) {
+                const size_t i0 = cnt2 * member / coopK, i1 = cnt2 * (member + 1) / coopK;
+                for (size_t i = i0 + tid; i < i1; i += NT) D2[i] = inf2;
+            }
             for (int w = tid; w < nwp; w += NT) { any0.st(w, 0u); any1.st(w, 0u); }
             if (tid == 0) {
                 ctl->qtail = 0;
@@ -267,16 +314,20 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->busyMax = 0;
                 ctl->busySum = 0;
                 ctl->maxOff = 0.0;
+                ctl->pubCnt = 0;
             }
         }
+        if (PART == 1 && coop && member == 0 && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 0);
         fence_wg();
         __syncthreads();
+        bool coopOk = true;
+        if (coop) coopOk = group_barrier(bar, coopK, epoch);   // every member's slice is +inf
         // lane offset: the source's distance to its nearest hub (host plan);
         // key = dist + (maxOff - off) lines the lanes up behind the hub
         const double off = (row >= 0 && bs.rowOff) ? as_global(bs.rowOff)[row] : 0.0;
         if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
         if (PART != 2 && gid == 0 && src >= 0) {
-            D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
+            if (member == 0) D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
             R[(size_t)src * LB + l] = 1.0;
             any0.set(src);
         }
@@ -302,7 +353,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         const long long tPh0 = dbg ? (long long)clock64() : 0;
         long long tPh1 = 0;
         int par = 0, phases = 0, repairs = 0;
-        bool failed = false;
+        bool failed = !coopOk;
         const int phaseCap = 8 * n + 1024;
         long long procs = 0, arcsDone = 0, lanesAct = 0;
         double bound = delta;
@@ -324,16 +375,73 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         for (;;) {   // phases + verification until the Bellman check holds
         if constexpr (PART != 2) {
         for (;;) {
+            if (failed) break;
             const Bits<GB> anyC = par ? any1 : any0;   // near
             const Bits<GB> anyF = par ? any0 : any1;   // far
+            int coopNear = 1;
+            if (coop) {
+                // publish this member's near bits (set by its relaxations,
+                // for any vertex) and its far scalars; after the barrier a
+                // member lists the merged near bits of the words it owns
+                // (w % K == member: hubs -- the lowest device ids -- spread)
+                if (myFar != INF_BITS) {
+                    atomicMin(&ctl->farMin, myFar);
+                    myFar = INF_BITS;
+                }
+                int cnt = 0;
+                for (int w = tid; w < nw; w += NT) {
+                    const uint32_t bits = anyC.ld(w);
+                    __hip_atomic_store(&pubNear[(size_t)member * nwp + w], bits, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    if (bits) { anyC.st(w, 0u); cnt += __popc(bits); }
+                }
+                if (cnt) atomicAdd(&ctl->pubCnt, cnt);
+                fence_wg();
+                __syncthreads();
+                if (tid == 0) {
+                    __hip_atomic_store(&pubS[member * 2], (unsigned long long)ctl->pubCnt |
+                                       ((unsigned long long)(ctl->farAny != 0) << 32),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&pubS[member * 2 + 1], ctl->farMin, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    ctl->pubCnt = 0;
+                }
+                if (!group_barrier(bar, coopK, epoch)) { failed = true; break; }
+                unsigned long long tot = 0, fmin = INF_BITS;
+                int fany = 0;
+                for (int k = 0; k < coopK; ++k) {
+                    const unsigned long long a =
+                        __hip_atomic_load(&pubS[k * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long f =
+                        __hip_atomic_load(&pubS[k * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    tot += a & 0xFFFFFFFFull;
+                    fany |= (int)(a >> 32);
+                    fmin = f < fmin ? f : fmin;
+                }
+                coopNear = tot != 0;
+                // the group's far state decides the bucket advance (uniform)
+                __syncthreads();
+                if (tid == 0 && !coopNear) {
+                    ctl->farAny = fany;
+                    ctl->farMin = fmin;
+                }
+            }
             // candidates = vertices with a near bit (consumed)
             // (hubs -- degree >= the engine's heavy threshold -- go to a list
             // of their own, processed by whole waves: one 16-lane group on a
             // hub's ~1000 arcs would set the phase's length)
-            for (int w = tid; w < nw; w += NT) {
-                uint32_t bits = anyC.ld(w);
+            for (int w = coop ? member + tid * coopK : tid; coopNear && w < nw; w += coop ? NT * coopK : NT) {
+                uint32_t bits;
+                if (coop) {
+                    bits = 0u;
+                    for (int k = 0; k < coopK; ++k)
+                        bits |= __hip_atomic_load(&pubNear[(size_t)k * nwp + w], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    bits = anyC.ld(w);
+                }
                 if (bits) {
-                    anyC.st(w, 0u);
+                    if (!coop) anyC.st(w, 0u);
                     uint32_t hv = bits & g.heavyBits[w];
                     bits &= ~hv;
                     if (bits) {
@@ -362,7 +470,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
             const int qn = ctl->qtail;
             const int hn = ctl->htail;
-            if (qn == 0 && hn == 0) {
+            if (qn == 0 && hn == 0 && (!coop || !coopNear)) {   // (coop: the group's near set)
                 // bucket settled: advance to the far set, or done
                 const int farAny = ctl->farAny;
                 const double fm = b2d(ctl->farMin);
@@ -629,7 +737,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const int vv = v0 + v < hi ? (fullPred ? v0 + v : ld_wg(&Q[v0 + v])) : -1;
                     vx[v] = vv;
                     if (vv >= 0) {
-                        dvb[v] = dec(ld_wg(&D[(size_t)vv * LB + l]));
+                        dvb[v] = dec(ld_wg(&D[(size_t)vv * DLB + dl]));
                         a0[v] = undirected ? g.rowPtr[vv] : g.inPtr[vv];
                         a1[v] = undirected ? g.rowPtr[vv + 1] : g.inPtr[vv + 1];
                     } else {
@@ -673,7 +781,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const unsigned long long t2 =
-                                dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]));
+                                dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * DLB + dl]));
                             du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
                         }
 #pragma unroll
@@ -703,7 +811,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const size_t e = (size_t)vv * LB + l;
                     const bool bad = !root[v] && mn[v] < dvb[v];
                     if (bad) {
-                        D[e] = enc_dirty(mn[v]);
+                        D[(size_t)vv * DLB + dl] = enc_dirty(mn[v]);
                         viol = 1;
                     }
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
@@ -767,7 +875,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         ++repairs;
         }   // verification loop
         if constexpr (PART == 1) {
-            if (tid == 0) as_global(bs.flags)[b] = failed ? 1 : 0;
+            if (coop) {                     // a failed member fails the batch (memory-side)
+                if (failed && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 1);
+            } else if (tid == 0) {
+                as_global(bs.flags)[b] = failed ? 1 : 0;
+            }
             break;
         }
         if (dbg) tPh2 = (long long)clock64();
@@ -804,7 +916,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 const int t = g.attached[j];
                 if (t != src) {
                     const size_t e = (size_t)t * LB + l;
-                    const unsigned long long dt = dec(ld_wg(&D[e]));
+                    const unsigned long long dt = dec(ld_wg(&D[(size_t)t * DLB + dl]));
                     if (dt != INF_BITS) {
                         int he = ld_wg(&H[e]);
                         double re = ld_wg(&R[e]);
@@ -944,7 +1056,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
                     } else {
                         const size_t e = (size_t)t * LB + l;
-                        const unsigned long long dt = dec(ld_wg(&D[e]));
+                        const unsigned long long dt = dec(ld_wg(&D[(size_t)t * DLB + dl]));
                         if (dt == INF_BITS) {
                             f |= F_UNREACHABLE;
                         } else {
@@ -1037,17 +1149,17 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 const int pe = ld_wg(&P[e]);
                 const bool am = pe >= 0 && (pe & TIE_AMB);
                 const size_t o = (size_t)sl * (size_t)tie.n + v;
-                tie.D[o] = b2d(dec(ld_wg(&D[e])));
+                tie.D[o] = b2d(dec(ld_wg(&D[(size_t)v * DLB + dl])));
                 tie.P[o] = pe;
                 if (am) {   // rare: re-derive the tied (minimum tight) predecessor distance
-                    const unsigned long long dv = dec(ld_wg(&D[e]));
+                    const unsigned long long dv = dec(ld_wg(&D[(size_t)v * DLB + dl]));
                     const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];
                     const int a1 = undirected ? g.rowPtr[v + 1] : g.inPtr[v + 1];
                     unsigned long long mt = INF_BITS;
                     for (int a = a0; a < a1; ++a) {
                         const int u = undirected ? g.col[a] : g.inCol[a];
                         const double w = undirected ? g.lat[a] : g.inLat[a];
-                        const unsigned long long du = dec(ld_wg(&D[(size_t)u * LB + l]));
+                        const unsigned long long du = dec(ld_wg(&D[(size_t)u * DLB + dl]));
                         if (du <= dv && d2b(b2d(du) + w) == dv && du < mt) mt = du;
                     }
                     if (mt != INF_BITS) thr = mt > thr ? mt : thr;
@@ -1065,7 +1177,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // 0 fast path, 1 full igraph-heap emulation, 2 + slot: early-stop
         // emulation with the exported tie data
         if (gid == 0 && row >= 0)
-            rowAmbig[(size_t)b * LB + l] =
+            rowAmbig[(size_t)b * DLB + dl] =
                 ((needMask >> l) & 1u) ? (uint8_t)(tieSlot[l] >= 0 ? 2 + tieSlot[l] : 1) : (uint8_t)0;
         if (dbg && tid == 0) {
             if (PART == 0) {
@@ -1163,7 +1275,15 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream, int part) {
     if (nBatches <= 0) return;
-    const int grid = nBatches < cfg.grid ? nBatches : cfg.grid;
+    int grid;
+    if (part == 1 && bs.coopK > 1) {          // groups of coopK consecutive workgroups
+        const int groups = nBatches < cfg.grid / bs.coopK ? nBatches : cfg.grid / bs.coopK;
+        grid = groups * bs.coopK;
+    } else {
+        const int items = part == 2 ? nBatches << bs.subShift : nBatches;
+        grid = items < cfg.grid ? items : cfg.grid;
+    }
+    if (grid <= 0) return;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (cfg.wpe >= 8)
         launch_wp<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid, part);

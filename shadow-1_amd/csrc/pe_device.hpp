@@ -80,6 +80,9 @@ struct Tuning {
     int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 1, batchWpe = 0;
     int relabel = 1;           // batched path: 1 = device ids by descending degree, 0 = as given
     int batchSplit = 1;        // batched path: relax / post as two kernels (predecessors on demand)
+    int batchDUncached = 0;    // batched path: dist arrays in uncached (memory-side coherent) memory
+    int batchCoop = 1;         // batched path: workgroups per batch in the relax kernel (1, 2, 4)
+    int batchPostSub = 0;      // batched path: post-kernel items per batch = 2^batchPostSub
     double batchDeltaFactor = 0.75, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
@@ -115,6 +118,15 @@ struct BatchScratch {
     int32_t* flags;          // split kernels: per batch of the round, 1 = phase cap hit
     const double* rowOff;    // [T] per table position: the source's distance to its
                              // batch hub (bucket key offset; null = no offsets)
+    // cooperative relax (small shards): coopK workgroups per batch, batches
+    // assigned statically to groups of coopK consecutive workgroups; shared
+    // state in uncached memory (the dist arrays too)
+    int32_t coopK;           // 1 = off (relax launches only)
+    uint32_t* pub;           // [group][member][words] published near bitmaps
+    unsigned long long* pubS;   // [group][member][2] near count | farAny << 32, farMin
+    int32_t* bar;            // [group * 16] barrier counters (zeroed per launch)
+    // post kernel: 2^subShift work items per batch of LB << subShift lanes
+    int32_t subShift;
 };
 
 struct BatchLaunch {

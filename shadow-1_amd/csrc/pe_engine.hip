@@ -77,6 +77,8 @@ struct Shard {
     bool batchReady = false;
     int32_t batchRound = 0;         // split kernels: batches per round (persisted dist arrays)
     int32_t batchSlots = 0;         // scratch slots allocated (no launch may exceed it)
+    int32_t coopK = 1;              // relax workgroups per batch (cooperative relax)
+    int32_t postSub = 0;            // post items per batch = 2^postSub (lanes split)
     int32_t* dBatchRows = nullptr;
     uint8_t* dBatchAmb = nullptr;
     TieBuf tie{};                   // early-stop tie rows (batched path)
@@ -168,6 +170,9 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_WPE", t.batchWpe);
     gi("SHDPE_RELABEL", t.relabel);
     gi("SHDPE_BATCH_SPLIT", t.batchSplit);
+    gi("SHDPE_BATCH_D_UNCACHED", t.batchDUncached);
+    gi("SHDPE_BATCH_COOP", t.batchCoop);
+    gi("SHDPE_BATCH_POST_SUB", t.batchPostSub);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -286,13 +291,16 @@ static int configure(ShdPe* pe, Shard* sh) {
     // LB 4 (32-B line pieces) stays a SHDPE_BATCH_LB option only
     b.lb = tu.batchLB;
     if (b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32)
-        b.lb = ((int64_t)sh->rowCount + 15) / 16 >= 2 * (int64_t)sh->numCUs ? 16 : 8;
+        b.lb = tu.batchCoop > 1 || ((int64_t)sh->rowCount + 15) / 16 >= 2 * (int64_t)sh->numCUs ? 16 : 8;
+    sh->coopK = tu.batchCoop == 2 || tu.batchCoop == 4 ? tu.batchCoop : 1;
+    sh->postSub = std::max(0, std::min(2, tu.batchPostSub));
+    if ((b.lb >> sh->postSub) < 4) sh->postSub = 0;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
     // control block, else in each slot's global scratch (gbits, LB 16)
     b.gbits = pe->batched && batch_lds_bytes((int)n, 8, false) > LDS ? 1 : 0;
-    if (b.gbits) b.lb = 16;
+    if (b.gbits) { b.lb = 16; sh->coopK = 1; }   // the cooperative relax keeps its bitmaps in LDS
     auto occupancy = [&](int wpe, int threads) {
         const int lds = batch_lds_bytes((int)n, wpe, b.gbits != 0);
         int per = 0;
@@ -823,7 +831,10 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
     const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
     const size_t grid = (size_t)std::max({sh->bcfg.grid, sh->bcfgAlt.grid, sh->bcfgAlt2.grid});
-    const size_t slots = std::min<size_t>({grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
+    // workgroups that can hold a slot: coopK per batch in the relax kernel,
+    // 2^postSub per batch in the post kernel
+    const size_t items = std::max<size_t>({1, nBatchesAll * (size_t)sh->coopK, nBatchesAll << sh->postSub});
+    const size_t slots = std::min<size_t>({grid, maxSlots, items});
     sh->bcfg.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfg.grid);
     if (sh->bcfgAlt.grid > 0) sh->bcfgAlt.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt.grid);
     if (sh->bcfgAlt2.grid > 0) sh->bcfgAlt2.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt2.grid);
@@ -844,7 +855,14 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->batchRound = (int32_t)roundB;
     sh->batchSlots = (int32_t)slots;
     void *D, *R, *H, *P, *q, *rows, *amb, *fl;
-    if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
+    if (pe->tu.batchDUncached || sh->coopK > 1) {   // memory-side coherent dist arrays
+        if (hipExtMallocWithFlags(&D, roundB * NS * LB * 8, hipDeviceMallocUncached) != hipSuccess)
+            return SHD_PE_ENOMEM;
+        sh->allocs.push_back(D);
+    } else if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8))) {
+        return rc;
+    }
+    if ((rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
         (rc = dev_alloc(sh, &q, slots * NS * 4 + 64)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
@@ -863,6 +881,29 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
         void* bits;
         if ((rc = dev_alloc(sh, &bits, slots * bitBytes))) return rc;
         sh->bsc.bits = (uint32_t*)bits;
+    }
+    sh->bsc.coopK = 1;
+    sh->bsc.subShift = 0;
+    sh->bsc.pub = nullptr;
+    sh->bsc.pubS = nullptr;
+    sh->bsc.bar = nullptr;
+    if (sh->coopK > 1) {
+        // published bitmaps / scalars / barrier counters, uncached: the
+        // members of a group may sit on different XCDs
+        const size_t nwp = (size_t)batch_bits_words(pe->hg.n) / 2;
+        void *pub, *pubS, *bar;
+        if (hipExtMallocWithFlags(&pub, slots * nwp * 4, hipDeviceMallocUncached) != hipSuccess)
+            return SHD_PE_ENOMEM;
+        sh->allocs.push_back(pub);
+        if (hipExtMallocWithFlags(&pubS, slots * 16, hipDeviceMallocUncached) != hipSuccess)
+            return SHD_PE_ENOMEM;
+        sh->allocs.push_back(pubS);
+        if (hipExtMallocWithFlags(&bar, slots * 64 + 64, hipDeviceMallocUncached) != hipSuccess)
+            return SHD_PE_ENOMEM;
+        sh->allocs.push_back(bar);
+        sh->bsc.pub = (uint32_t*)pub;
+        sh->bsc.pubS = (unsigned long long*)pubS;
+        sh->bsc.bar = (int32_t*)bar;
     }
     sh->bsc.rowOff = nullptr;
     if (!pe->rowOff.empty()) {
@@ -1085,13 +1126,19 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 // (the post kernel may run another variant: bcfgPost)
                 BatchLaunch post = sh->bcfgPost.grid > 0 ? sh->bcfgPost : sh->bcfg;
                 post.grid = std::min(post.grid, sh->batchSlots);
+                post.lb >>= sh->postSub;            // lanes per post workgroup
                 for (int32_t r0 = 0; r0 < nB; r0 += sh->batchRound) {
                     const int32_t rn = std::min(sh->batchRound, nB - r0);
                     const size_t ro = (size_t)r0 * LB;
                     if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[0], sh->stream));
                     for (int part = 1; part <= 2; ++part) {
                         HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
-                        launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows + ro, rn,
+                        BatchScratch bs = sh->bsc;
+                        bs.coopK = part == 1 ? sh->coopK : 1;
+                        bs.subShift = part == 2 ? sh->postSub : 0;
+                        if (bs.coopK > 1)
+                            HIPCHK(hipMemsetAsync(bs.bar, 0, (size_t)sh->batchSlots * 64 + 64, sh->stream));
+                        launch_batch_rows(sh->dg, sh->tab, bs, sh->dBatchRows + ro, rn,
                                           sh->dBatchAmb + ro, part == 1 ? relax : post,
                                           sh->dDbg ? sh->dDbg + 16 * r0 : nullptr, sh->dTie, sh->stream, part);
                         if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[part], sh->stream));

@@ -36,6 +36,19 @@ for st in ${STAGES:-tests bench}; do
     # rank 0's shard at N = $SHARD_NS
     SHDPE_DEBUG=1 timeout -k 10 400 python3 -u tools/shard_time.py ${SHARD_WL:-c4} ${SHARD_NS:-8} > $OUT/sharddbg.txt 2> $OUT/sharddbg.err || { tail -20 $OUT/sharddbg.err; exit 1; }
     cat $OUT/sharddbg.txt; grep "shdpe\] .*batch" $OUT/sharddbg.err | tail -12 ;;
+  ab)
+    # same-box A/B of library builds (tools/build_variant.sh): LIBS="new x y"
+    # -> shadow-1_amd/libshdpe_<x>.so (new = the in-tree libshdpe.so), REPS
+    # rounds alternating, quick C4 lines
+    for wl in ${WLS//,/ }; do
+      for rep in $(seq 1 ${REPS:-2}); do
+        for lib in ${LIBS:-new}; do
+          L=shadow-1_amd/libshdpe.so; [ $lib != new ] && L=shadow-1_amd/libshdpe_$lib.so
+          SHDPE_LIB=$R/$L timeout -k 10 300 python3 -u bench.py --workload $wl --steps 3 --warmup 1 $QUICK > $OUT/ab_${wl}_$lib.json 2> $OUT/ab_${wl}_$lib.err || { tail -20 $OUT/ab_${wl}_$lib.err; exit 1; }
+          line $OUT/ab_${wl}_$lib.json "$wl $lib #$rep"
+        done
+      done
+    done ;;
   bench)
     for wl in ${WLS//,/ }; do
       timeout -k 10 300 python3 -u bench.py --workload $wl --steps ${STEPS:-3} --warmup 1 $QUICK > $OUT/bench_$wl.json 2> $OUT/bench_$wl.err || { tail -20 $OUT/bench_$wl.err; exit 1; }
