@@ -208,7 +208,7 @@ __device__ __forceinline__ bool group_barrier(int* bar, int K, int& epoch) {
         int good = 1;
         for (long long spin = 0;; ++spin) {
             if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-            if (spin > (1ll << 24)) { good = 0; break; }
+            if (spin > (1ll << 20)) { good = 0; break; }   // ~1 s
             __builtin_amdgcn_s_sleep(2);
         }
         ok = good;
