@@ -588,6 +588,7 @@ def test_batched_cooperative_relax(E, oracle_mod, monkeypatch, coop, sub, wpe, c
     slices of each batch; bit-exact with the oracle, tie rows included."""
     monkeypatch.setenv("SHDPE_BATCH_COOP", str(coop))
     monkeypatch.setenv("SHDPE_BATCH_POST_SUB", str(sub))
+    monkeypatch.setenv("SHDPE_BATCH_LB", "16")
     monkeypatch.setenv("SHDPE_BATCH_WPE", str(wpe))
     if case == "power_law":
         top = G.power_law(8000, m=3, seed=16)
