@@ -75,16 +75,18 @@ struct alignas(16) BCtrl {
     int pubCnt;       // cooperative relax: near bits published this phase
 };
 
-// Entry encoding of the [v][LB] distance array: (f64 bits << 1) | clean.
+// Entry encoding of the [v][LB] distance array: (f64 bits << 1) | dirty.
 // Positive doubles have bit 63 clear, so the shift loses nothing and the u64
 // order of encodings is the order of distances: an atomic min with a dirty
-// (clean = 0) encoding of a smaller distance always wins, an equal or larger
-// one never changes the distance.  A processor marks the value it relaxed
-// clean with a CAS, which fails (leaving the entry dirty) if an improvement
-// landed in between.
-__device__ __forceinline__ unsigned long long enc_dirty(unsigned long long bits) { return bits << 1; }
+// encoding of a smaller distance always wins, an equal or larger one never
+// changes the entry (an equal distance does not re-dirty a clean entry:
+// clean = bit 0 clear is the smaller encoding).  A processor marks the value
+// it relaxed clean with a no-return atomic min of e & ~1: if an improvement
+// landed in between, its encoding is below e & ~1 and stays, dirty.
+__device__ __forceinline__ unsigned long long enc_dirty(unsigned long long bits) { return (bits << 1) | 1ull; }
 __device__ __forceinline__ unsigned long long dec(unsigned long long e) { return e >> 1; }
-constexpr unsigned long long INF_ENC = (INF_BITS << 1) | 1ull;
+__device__ __forceinline__ bool is_dirty(unsigned long long e) { return (e & 1ull) != 0; }
+constexpr unsigned long long INF_ENC = INF_BITS << 1;   // +inf, clean
 
 // (perturbation variants of these three -- plain stores, doubled atomics,
 // doubled reads -- are patches under tools/variants/, built by
@@ -99,9 +101,7 @@ __device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, in
 }
 
 __device__ __forceinline__ void mark_clean(unsigned long long* p, unsigned long long e) {
-    unsigned long long expect = e;
-    (void)__hip_atomic_compare_exchange_strong(p, &expect, e | 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_min(p, e & ~1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Pending bitmaps (one bit per vertex, near + far sets): in LDS when both
@@ -503,7 +503,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const unsigned long long e0 = ld_wg(pu);
                     const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
                     const double k0 = b2d(dec(e0)) + sh;
-                    const bool dirty = !(e0 & 1ull);
+                    const bool dirty = is_dirty(e0);
                     const bool below = dirty && k0 < bound;
                     const bool act = EAGER ? dirty && __ballot(below) >> gbase & LBMASK : below;
                     const bool defer = dirty && !act;
@@ -601,7 +601,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
                     const double k0 = b2d(dec(db[v])) + sh;
-                    const bool dirty = !(db[v] & 1ull);
+                    const bool dirty = is_dirty(db[v]);
                     const bool below = dirty && k0 < bound;
                     const bool act = EAGER ? dirty && __ballot(below) >> gbase & LBMASK : below;
                     const bool defer = dirty && !act;
