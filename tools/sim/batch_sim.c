@@ -18,6 +18,10 @@ typedef struct {
     double touched;     // distinct (vertex, phase) pairs relaxed into (any lane, improving or not)
     double improving;   // arc visits with at least one improving lane
     double laneImp;     // improving lane relaxations
+    double skippable;   // arc visits whose head had every lane's key below the last closed
+                        // bucket bound (final for all lanes: the D-line read is avoidable)
+    double skip2;       // ... and known to be so through a record made when the head was last
+                        // processed with all lanes' keys below that phase's bound (2-bitmap scheme)
 } SimOut;
 
 // vkey (optional, [nBatch][n]): a per-VERTEX bucket key replacing every
@@ -35,6 +39,8 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     int32_t* stamp = malloc(sizeof(int32_t) * n);
     uint64_t* hpend = calloc(n, 8);   // lanes whose heavy arcs wait for their bucket to settle
     for (int v = 0; v < n; ++v) stamp[v] = -1;
+    uint8_t* recP = calloc(n, 1);   // all lanes below the bound when last processed (this bucket)
+    uint8_t* recF = calloc(n, 1);   // ... in a closed bucket: final
     int32_t gphase = 0;
     if (!D || !pend || !nextp || !q) return -1;
     memset(out, 0, sizeof(*out));
@@ -48,6 +54,8 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
         memset(dirty, 0, 8 * (size_t)n);
         memset(farp, 0, n);
         memset(hpend, 0, 8 * (size_t)n);
+        memset(recP, 0, n);
+        memset(recF, 0, n);
         double farMin = INFINITY;
         double maxOff = 0;
         for (int l = 0; l < LB; ++l) {
@@ -57,6 +65,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
             pend[s[l]] = 1;
             if (off[l] > maxOff) maxOff = off[l];
         }
+        double closed = -INFINITY;   // keys below it are final
         double bound = -maxOff + delta;
         // start at the bucket of the smallest source key
         {
@@ -114,6 +123,8 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 farMin = INFINITY;
                 double nb = (floor(mn / delta) + 1.0) * delta;
                 if (!(mn < nb)) nb = mn + delta;
+                closed = bound;
+                for (int v = 0; v < n; ++v) if (recP[v]) { recP[v] = 0; recF[v] = 1; }
                 bound = nb;
                 memcpy(pend, farp, n);
                 memset(farp, 0, n);
@@ -157,6 +168,12 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 if (!act) continue;
                 dirty[u] &= ~act;
                 out->procs += 1;
+                {
+                    int all = 1;
+                    for (int l = 0; l < LB; ++l)
+                        if (s[l] >= 0 && !(du[l] != INFINITY && KEY(u, l, du[l]) < bound)) all = 0;
+                    if (all) recP[u] = 1;
+                }
                 out->lanesAct += __builtin_popcountll(act);
                 if (farMode & 4) hpend[u] |= act;
                 for (int a = rowPtr[u]; a < rowPtr[u + 1]; ++a) {
@@ -164,6 +181,15 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                     const double w = lat[a];
                     if ((farMode & 4) && w >= delta) continue;
                     out->arcs += 1;
+                    {
+                        int all = 1;
+                        for (int l = 0; l < LB; ++l) {
+                            const double dx = D[(size_t)x * LB + l];
+                            if (s[l] >= 0 && !(dx != INFINITY && KEY(x, l, dx) < closed)) all = 0;
+                        }
+                        out->skippable += all;
+                        out->skip2 += recF[x];
+                    }
                     if (stamp[x] != gphase) { stamp[x] = gphase; out->touched += 1; }
                     int anyImp = 0;
                     for (int l = 0; l < LB; ++l) {
@@ -204,5 +230,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     free(farp);
     free(stamp);
     free(hpend);
+    free(recP);
+    free(recF);
     return 0;
 }
