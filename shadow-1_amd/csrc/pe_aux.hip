@@ -130,15 +130,22 @@ __global__ __launch_bounds__(256) void k_pairs(DevGraph g0, const int32_t* __res
 
 // _topology_isComplete: every vertex's incident count (self-loop counted
 // twice undirected, then corrected by one) must reach n.  Minimum count.
-__global__ __launch_bounds__(256) void k_incident_min(DevGraph g0, int32_t* out) {
+// Multigraphs pass the host's per-vertex edge counts (merged rows hold one
+// arc per neighbour, the reference counts every parallel edge).
+__global__ __launch_bounds__(256) void k_incident_min(DevGraph g0, const int32_t* __restrict__ edgeCount,
+                                                      int32_t* out) {
     const DevGraph g = global_view(g0);
     const int v = blockIdx.x * 256 + threadIdx.x;
     int c = INT32_MAX;
     if (v < g.n) {
-        c = g.rowPtr[v + 1] - g.rowPtr[v];
-        // a loop counts once directed; twice undirected, minus the one
-        // correction of :505-519 -- once either way
-        if (g.hasSelf[v]) c += 1;
+        if (edgeCount) {
+            c = edgeCount[v];
+        } else {
+            c = g.rowPtr[v + 1] - g.rowPtr[v];
+            // a loop counts once directed; twice undirected, minus the one
+            // correction of :505-519 -- once either way
+            if (g.hasSelf[v]) c += 1;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c = min(c, __shfl_xor(c, o, 64));
@@ -193,9 +200,9 @@ void launch_pairs(const DevGraph& g, const int32_t* dSrc, const int32_t* dDst, i
                        dRel, dFlags);
 }
 
-void launch_incident_min(const DevGraph& g, int32_t* dOut, void* stream) {
+void launch_incident_min(const DevGraph& g, const int32_t* dEdgeCount, int32_t* dOut, void* stream) {
     hipLaunchKernelGGL(k_incident_min, dim3((g.n + 255) / 256), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), g, dOut);
+                       reinterpret_cast<hipStream_t>(stream), g, dEdgeCount, dOut);
 }
 
 }  // namespace shdpe

@@ -234,7 +234,7 @@ void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, 
 // mode 0 direct paths (lat, rel, flags), mode 1 adjacency (flags = 0 / 1)
 void launch_pairs(const DevGraph& g, const int32_t* dSrc, const int32_t* dDst, int64_t count,
                   int mode, double* dLat, double* dRel, uint8_t* dFlags, void* stream);
-void launch_incident_min(const DevGraph& g, int32_t* dOut, void* stream);
+void launch_incident_min(const DevGraph& g, const int32_t* dEdgeCount, int32_t* dOut, void* stream);
 // dense path (pe_dense.hip)
 void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int64_t nArcs,
                         void* stream);

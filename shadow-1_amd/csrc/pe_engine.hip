@@ -205,7 +205,7 @@ extern "C" const char* shd_pe_strerror(int code) {
         case SHD_PE_ENODEV: return "no usable gfx950 device";
         case SHD_PE_EUNREACHABLE: return "target unreachable";
         case SHD_PE_ENOSELFLOOP: return "self-loop (s,s) missing";
-        case SHD_PE_EMULTI: return "parallel edges (multigraph) are not supported";
+        case SHD_PE_EMULTI: return "multigraph whose newest parallel edge is not a fastest one (unsupported)";
         case SHD_PE_EHIP: return "HIP runtime error";
         case SHD_PE_ENOTATTACHED: return "vertex is not attached";
         case SHD_PE_ENOEDGE: return "no edge between the vertices";
@@ -2205,7 +2205,12 @@ extern "C" int shd_pe_is_complete_device(ShdPe* pe, int32_t* isComplete) {
     if (hipMalloc(&b.p[0], 4)) return SHD_PE_ENOMEM;
     const int32_t init = INT32_MAX;
     HIPCHK(hipMemcpyAsync(b.p[0], &init, 4, hipMemcpyHostToDevice, sh->stream));
-    launch_incident_min(sh->dgAux, (int32_t*)b.p[0], sh->stream);
+    const std::vector<int32_t>& ec = pe->hg.edgeCount;    // multigraphs: edge counts
+    if (!ec.empty()) {
+        if (hipMalloc(&b.p[1], ec.size() * 4)) return SHD_PE_ENOMEM;
+        HIPCHK(hipMemcpyAsync(b.p[1], ec.data(), ec.size() * 4, hipMemcpyHostToDevice, sh->stream));
+    }
+    launch_incident_min(sh->dgAux, ec.empty() ? nullptr : (const int32_t*)b.p[1], (int32_t*)b.p[0], sh->stream);
     HIPCHK(hipGetLastError());
     int32_t mn = 0;
     HIPCHK(hipMemcpyAsync(&mn, b.p[0], 4, hipMemcpyDeviceToHost, sh->stream));

@@ -6,7 +6,21 @@
 // incidence list of v (igraph_incident, mode OUT; undirected -> ALL) is
 // [oi: from==v sorted by to][ii: to==v sorted by from] with undirected edges
 // stored from=max(a,b) -- i.e. ascending neighbour id, self-loop in place
-// (SURVEY.md Appendix A.1-A.2).  Multigraphs are rejected (SHD_PE_EMULTI).
+// (SURVEY.md Appendix A.1-A.2).
+//
+// Multigraphs: igraph lists parallel edges to one neighbour consecutively
+// (newest first), Dijkstra relaxes each of them, and the fold reads the edge
+// igraph_get_eid returns -- the NEWEST (highest id) parallel edge
+// (type_indexededgelist.c BINSEARCH over an index sorted with descending ids
+// among equals; oracle/pe_oracle.c orc_get_eid).  Consecutive relaxations of
+// one neighbour by w1, w2, ... leave the same distances, heap array and
+// parent vertex as one relaxation by min(w) (a second shift_up continues the
+// first over the same ancestor chain), so a group of parallel edges becomes
+// ONE arc with the group's minimum latency and the newest edge's reliability.
+// The path latency the reference reports is the fold of get_eid latencies,
+// which equals the Dijkstra distance only when the newest edge of every group
+// is a fastest one; other multigraphs are rejected (SHD_PE_EMULTI).  Several
+// self-loops on a vertex: the same rule (the newest one is the (v, v) edge).
 #include "pe_graph.hpp"
 
 #include <algorithm>
@@ -50,12 +64,13 @@ static void par_chunks(int64_t n, int nChunks, int64_t work, F f) {
     for (auto& x : th) x.join();
 }
 
-// Sort each row by neighbour id (igraph incidence order); a repeated
-// neighbour is a parallel edge -> SHD_PE_EMULTI.
-static int sort_rows(int32_t n, const std::vector<int32_t>& ptr, hvec<int32_t>& colv,
-                     hvec<double>& latv, hvec<double>& relv) {
+// Sort each row by neighbour id (igraph incidence order), parallel edges of
+// one neighbour in edge-id order (the fill order); returns whether any row
+// has a repeated neighbour (a multigraph).
+static bool sort_rows(int32_t n, const std::vector<int32_t>& ptr, hvec<int32_t>& colv,
+                      hvec<double>& latv, hvec<double>& relv) {
     const int nc = 64;
-    std::vector<int> rcs(nc, SHD_PE_OK);
+    std::vector<uint8_t> multi(nc, 0);
     par_chunks(n, nc, (int64_t)colv.size(), [&](int c, int64_t v0, int64_t v1) {
         std::vector<std::pair<int32_t, int32_t>> tmp;
         std::vector<double> l2, r2;
@@ -69,7 +84,7 @@ static int sort_rows(int32_t n, const std::vector<int32_t>& ptr, hvec<int32_t>& 
             for (int32_t a = b; a < e; ++a) tmp.emplace_back(colv[a], a);
             std::sort(tmp.begin(), tmp.end());
             for (size_t k = 1; k < tmp.size(); ++k)
-                if (tmp[k].first == tmp[k - 1].first) { rcs[c] = SHD_PE_EMULTI; return; }
+                if (tmp[k].first == tmp[k - 1].first) multi[c] = 1;
             l2.resize(tmp.size());
             r2.resize(tmp.size());
             for (size_t k = 0; k < tmp.size(); ++k) {
@@ -83,8 +98,37 @@ static int sort_rows(int32_t n, const std::vector<int32_t>& ptr, hvec<int32_t>& 
             }
         }
     });
-    for (int r : rcs)
-        if (r) return r;
+    for (uint8_t x : multi)
+        if (x) return true;
+    return false;
+}
+
+// One arc per (vertex, neighbour): the newest parallel edge (the last of its
+// group in edge-id order) with the group's minimum latency, which must be the
+// newest edge's own (see the header); rows compacted in place.
+static int merge_parallel(int32_t n, std::vector<int32_t>& ptr, hvec<int32_t>& colv, hvec<double>& latv,
+                          hvec<double>& relv) {
+    int32_t w = 0;
+    for (int32_t v = 0; v < n; ++v) {
+        const int32_t b = ptr[v], e = ptr[v + 1];
+        ptr[v] = w;
+        for (int32_t a = b; a < e;) {
+            int32_t z = a + 1;
+            double mn = latv[a];
+            while (z < e && colv[z] == colv[a]) { mn = std::min(mn, latv[z]); ++z; }
+            const int32_t newest = z - 1;
+            if (latv[newest] != mn) return SHD_PE_EMULTI;
+            colv[w] = colv[newest];
+            latv[w] = latv[newest];
+            relv[w] = relv[newest];
+            ++w;
+            a = z;
+        }
+    }
+    ptr[n] = w;
+    colv.resize(w);
+    latv.resize(w);
+    relv.resize(w);
     return SHD_PE_OK;
 }
 
@@ -136,17 +180,24 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     });
     int64_t bad = INT64_MAX;
     for (int64_t x : firstBad) bad = std::min(bad, x);
+    // self-loops in edge order: the newest one of a vertex is its (v, v)
+    // edge; nSelf counts them for the completeness rule
+    std::vector<int32_t> nSelf(n, 0);
+    std::vector<double> selfMin(n, INFINITY);
     for (int c = 0; c < NC; ++c) {
         for (int64_t e : loops[c]) {
             if (e > bad) break;
             const int32_t a = d->edgeFrom[e];
-            if (g->hasSelf[a]) return SHD_PE_EMULTI;
             g->hasSelf[a] = 1;
+            nSelf[a]++;
+            selfMin[a] = std::min(selfMin[a], d->edgeLatency[e]);
             g->selfLat[a] = d->edgeLatency[e];
             g->selfRel[a] = 1.0 - d->edgePacketLoss[e];                 // :437
         }
     }
     if (bad != INT64_MAX) return SHD_PE_EINVAL;
+    for (int32_t v = 0; v < n; ++v)
+        if (nSelf[v] > 1 && g->selfLat[v] != selfMin[v]) return SHD_PE_EMULTI;
     // row pointers; chunk c writes row v from offset rowPtr[v] + (arcs of v
     // in chunks < c): every row keeps edge-id order, as the serial fill
     g->rowPtr.assign(n + 1, 0);
@@ -183,19 +234,27 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     });
     cnt.clear();
     cnt.shrink_to_fit();
-    int rc = sort_rows(n, g->rowPtr, g->col, g->lat, g->rel);
-    if (rc) return rc;
+    // incident edge counts before parallel edges merge (_topology_isComplete
+    // counts edges, not neighbours)
+    std::vector<int32_t> rawDeg;
+    if (sort_rows(n, g->rowPtr, g->col, g->lat, g->rel)) {
+        rawDeg.resize(n);
+        for (int32_t v = 0; v < n; ++v) rawDeg[v] = g->rowPtr[v + 1] - g->rowPtr[v];
+        const int rc = merge_parallel(n, g->rowPtr, g->col, g->lat, g->rel);
+        if (rc) return rc;
+    }
+    const int64_t nArcsM = g->rowPtr[n];
 
-    g->outToIn.resize(nArcs);
+    g->outToIn.resize(nArcsM);
     if (g->directed) {
         // IN CSR sorted by source id
         std::vector<int32_t> cntIn(n + 1, 0);
-        for (int64_t a = 0; a < nArcs; ++a) cntIn[g->col[a] + 1]++;
+        for (int64_t a = 0; a < nArcsM; ++a) cntIn[g->col[a] + 1]++;
         for (int32_t v = 0; v < n; ++v) cntIn[v + 1] += cntIn[v];
         g->inPtr = cntIn;
-        g->inCol.resize(nArcs);
-        g->inLat.resize(nArcs);
-        g->inRel.resize(nArcs);
+        g->inCol.resize(nArcsM);
+        g->inLat.resize(nArcsM);
+        g->inRel.resize(nArcsM);
         std::vector<int32_t> fill(cntIn.begin(), cntIn.end() - 1);
         for (int32_t u = 0; u < n; ++u) {               // rows visited in source order
             for (int32_t a = g->rowPtr[u]; a < g->rowPtr[u + 1]; ++a) {
@@ -208,7 +267,7 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     } else {
         // reverse arc of u->v: position of u in v's sorted row
         std::vector<int> rcs(64, SHD_PE_OK);
-        par_chunks(n, 64, nArcs * 16, [&](int c, int64_t u0, int64_t u1) {
+        par_chunks(n, 64, nArcsM * 16, [&](int c, int64_t u0, int64_t u1) {
             for (int64_t u = u0; u < u1; ++u) {
                 for (int32_t a = g->rowPtr[u]; a < g->rowPtr[u + 1]; ++a) {
                     const int64_t rev = g->findArc(g->col[a], (int32_t)u);
@@ -220,20 +279,25 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
         for (int r : rcs)
             if (r) return r;
     }
-    // _topology_isComplete (topology.c:450-552): incident count (undirected
-    // self-loop counted twice, then corrected by one) must reach vcount.
+    // _topology_isComplete (topology.c:450-552): incident EDGE count (parallel
+    // edges each; an undirected self-loop counted twice, then one correction
+    // when get_eid(v, v) exists) must reach vcount.
     bool complete = true;
-    for (int32_t v = 0; v < n && complete; ++v) {
-        int64_t c = (int64_t)(g->rowPtr[v + 1] - g->rowPtr[v]);
-        c += g->hasSelf[v] ? (g->directed ? 1 : 2) : 0;
+    const bool multi = !rawDeg.empty() || *std::max_element(nSelf.begin(), nSelf.end()) > 1;
+    if (multi) g->edgeCount.resize(n);
+    for (int32_t v = 0; v < n; ++v) {
+        int64_t c = rawDeg.empty() ? (int64_t)(g->rowPtr[v + 1] - g->rowPtr[v]) : rawDeg[v];
+        c += g->directed ? nSelf[v] : 2 * (int64_t)nSelf[v];
         if (!g->directed && g->hasSelf[v]) c -= 1;
         if (c < n) complete = false;
+        if (multi) g->edgeCount[v] = (int32_t)std::min<int64_t>(c, INT32_MAX);
+        else if (!complete) break;
     }
     g->isComplete = complete;
     // mean arc latency (bucket width): fixed 64-chunk partial sums added in
     // order, so the value does not depend on the thread count
     std::vector<double> part(64, 0.0), pmin(64, INFINITY);
-    par_chunks(nArcs, 64, nArcs, [&](int c, int64_t a0, int64_t a1) {
+    par_chunks(nArcsM, 64, nArcsM, [&](int c, int64_t a0, int64_t a1) {
         double s = 0.0, mn = INFINITY;
         for (int64_t a = a0; a < a1; ++a) { s += g->lat[a]; mn = std::min(mn, g->lat[a]); }
         part[c] = s;
@@ -242,8 +306,8 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     double sum = 0.0, mn = INFINITY;
     for (double x : part) sum += x;
     for (double x : pmin) mn = std::min(mn, x);
-    g->minArcLatency = nArcs ? mn : 0.0;
-    g->meanArcLatency = nArcs ? sum / (double)nArcs : 1.0;
+    g->minArcLatency = nArcsM ? mn : 0.0;
+    g->meanArcLatency = nArcsM ? sum / (double)nArcsM : 1.0;
     return SHD_PE_OK;
 }
 

@@ -45,12 +45,17 @@ struct HostGraph {
     std::vector<double> selfLat, selfRel;
     std::vector<uint8_t> hasSelf;
     bool isComplete = false;
+    // multigraphs only (empty otherwise): per vertex the incident EDGE count
+    // _topology_isComplete compares with vcount (parallel edges each, the
+    // undirected self-loop correction applied) -- the merged rows undercount
+    std::vector<int32_t> edgeCount;
     double meanArcLatency = 0.0;
     double minArcLatency = 0.0;     // smallest non-loop arc latency (0: no arcs)
 
     int64_t nArcs() const { return (int64_t)col.size(); }
-    // igraph_get_eid(from,to) restricted to simple graphs: arc index into the
-    // OUT arrays, -2 for the self-loop, -1 for none.
+    // igraph_get_eid(from,to): arc index into the OUT arrays (parallel edges
+    // are merged into the arc of the newest one), -2 for the self-loop, -1
+    // for none.
     int64_t findArc(int32_t from, int32_t to) const;
 };
 

@@ -198,6 +198,49 @@ def minus_one_edge(top: Topology, seed: int = 0) -> Topology:
                     name=top.name + "_minus1")
 
 
+def with_parallel_edges(top: Topology, frac: float, seed: int, consistent: bool = True,
+                        loops: bool = True) -> Topology:
+    """A multigraph: parallel copies of a fraction of the edges (and of the
+    self-loops) appended after the originals, so each copy is the NEWEST edge
+    of its group -- the one igraph_get_eid returns (oracle orc_get_eid).  With
+    `consistent` every copy is also a fastest edge of its group (equal latency
+    with another loss, or faster); otherwise one copy is slower than the edge
+    it duplicates (the engine rejects that, SHD_PE_EMULTI)."""
+    rng = np.random.default_rng(seed)
+    cand = np.flatnonzero(top.src != top.dst)
+    if loops:
+        cand = np.concatenate([cand, np.flatnonzero(top.src == top.dst)])
+    pick = rng.choice(cand, size=max(1, int(frac * cand.shape[0])), replace=False)
+    src, dst = [top.src], [top.dst]
+    lat, loss = [top.latency], [top.loss]
+    cur = {}
+    for rep in range(2):                        # some groups get two copies
+        sel = pick if rep == 0 else pick[rng.random(pick.shape[0]) < 0.3]
+        l = np.array([cur.get(int(k), top.latency[k]) for k in sel])
+        faster = rng.random(sel.shape[0]) < 0.5
+        l = np.where(faster, l * rng.uniform(0.5, 1.0, size=sel.shape[0]), l)
+        for k, x in zip(sel, l):
+            cur[int(k)] = float(x)
+        src.append(top.src[sel]); dst.append(top.dst[sel])
+        # undirected copies sometimes list the endpoints the other way round
+        if not top.directed:
+            flip = rng.random(sel.shape[0]) < 0.5
+            src[-1], dst[-1] = np.where(flip, top.dst[sel], top.src[sel]), np.where(flip, top.src[sel], top.dst[sel])
+        lat.append(l); loss.append(rng.uniform(0.0, 0.05, size=sel.shape[0]))
+    lat = np.concatenate(lat)
+    if not consistent:
+        lat[top.m] = top.latency[pick[0]] * 1.5   # the newest copy of pick[0] is slower
+        if top.m + pick.shape[0] < lat.shape[0]:
+            keep = np.ones(lat.shape[0], bool)
+            keep[top.m + pick.shape[0]:] = False   # no second copies: pick[0]'s slow copy stays newest
+            return Topology(n=top.n, directed=top.directed, src=np.concatenate(src)[keep],
+                            dst=np.concatenate(dst)[keep], latency=lat[keep],
+                            loss=np.concatenate(loss)[keep], vloss=top.vloss, name=top.name + "_multi_bad")
+    return Topology(n=top.n, directed=top.directed, src=np.concatenate(src), dst=np.concatenate(dst),
+                    latency=lat, loss=np.concatenate(loss), vloss=top.vloss,
+                    name=top.name + ("_multi" if consistent else "_multi_bad"))
+
+
 def sample_attached(n: int, k: int, seed: int) -> np.ndarray:
     """Attached vertices (``verticesWithAttachedHosts``), sorted."""
     if k >= n:

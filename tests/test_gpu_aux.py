@@ -43,6 +43,8 @@ def _graphs():
     yield "directed_vloss", G.random_sparse(500, 6, seed=4, directed=True, vloss=True)
     yield "missing_loops", _drop_some_loops(G.random_sparse(600, 5, seed=5, quantum=5.0), 1)
     yield "power_law", G.power_law(5000, m=3, seed=7, quantum=0.5)
+    yield "multigraph", G.with_parallel_edges(G.random_sparse(500, 6, seed=12, vloss=True, quantum=5.0), 0.3, seed=5)
+    yield "multigraph_directed", G.with_parallel_edges(G.random_sparse(400, 6, seed=13, directed=True), 0.3, seed=6)
 
 
 @pytest.mark.parametrize("name,top", list(_graphs()), ids=[n for n, _ in _graphs()])
@@ -93,7 +95,9 @@ def test_is_complete_device(E, oracle_mod):
     top = Topology.load_npz(os.path.join(ROOT, "tests", "golden", "shipped_topology.npz"),
                             name="shipped")
     for t in (top, G.minus_one_edge(top, seed=3), G.dense(300, seed=2),
-              G.dense(300, seed=2, drop_edge=True), G.random_sparse(200, 4, seed=1)):
+              G.dense(300, seed=2, drop_edge=True), G.random_sparse(200, 4, seed=1),
+              G.with_parallel_edges(G.dense(100, seed=2, drop_edge=True), 0.2, seed=3),
+              G.with_parallel_edges(G.random_sparse(200, 4, seed=1), 0.5, seed=4)):
         eng = E.Engine(t, np.arange(min(t.n, 32), dtype=np.int32))
         og = oracle_mod.OracleGraph(t)
         assert eng.is_complete_device() == og.is_complete() == bool(eng.stats()["isComplete"])

@@ -197,11 +197,87 @@ def test_complete_graph_direct_rows(E, oracle_mod):
 
 
 def test_multigraph_rejected(E):
+    """The newest parallel edge (igraph_get_eid's, the one the reference folds)
+    slower than an older one: the table's latency would differ from the
+    distance -- rejected."""
     top = Topology(3, False, np.array([0, 1, 0, 0, 1, 2]), np.array([1, 0, 0, 2, 1, 2]),
-                   np.ones(6), np.zeros(6))
+                   np.array([1.0, 2.0, 1.0, 1.0, 1.0, 1.0]), np.zeros(6))
     with pytest.raises(E.EngineError) as ei:
         E.Engine(top, np.arange(3))
     assert ei.value.code == E.EMULTI
+
+
+@pytest.mark.parametrize("directed", [False, True], ids=["undirected", "directed"])
+@pytest.mark.parametrize("quantum", [0.0, 5.0], ids=["tiefree", "quantised"])
+@pytest.mark.parametrize("force", [0, 5], ids=["sparse", "batched"])
+def test_multigraph_rows(E, oracle_mod, directed, quantum, force):
+    """Multigraphs (topology.c:417-420: igraph_get_eid picks the newest parallel
+    edge for the fold; Dijkstra relaxes every parallel edge in incidence order,
+    newest first): parallel copies of 30% of the edges and self-loops, each
+    copy the newest of its group and a fastest one, some groups of three,
+    vertex loss; every row bit-exact against the oracle's igraph-faithful
+    run over the unmerged edge list, tie rows through the exact kernel."""
+    base = G.random_sparse(400, 5, seed=41 + int(directed), directed=directed, quantum=quantum, vloss=True)
+    top = G.with_parallel_edges(base, 0.3, seed=7)
+    assert top.m > base.m + 100
+    st = _check_engine(E, oracle_mod, top, np.arange(0, 400, 3, dtype=np.int32), force=force)
+    if force == 5:
+        assert st["mode"] == 1
+    if quantum > 0:
+        assert st["rowsExact"] > 0          # tie rows went through the igraph heap emulation
+
+
+def test_multigraph_complete_direct_rows(E, oracle_mod):
+    """Complete multigraphs take the direct rows: every entry is the newest
+    parallel edge's (latency, reliability), as _topology_lookupDirectPath
+    reads it through igraph_get_eid (topology.c:1877-1927)."""
+    top = G.with_parallel_edges(G.dense(60, seed=5), 0.3, seed=9)
+    og = oracle_mod.OracleGraph(top)
+    eng = E.Engine(top, np.arange(top.n, dtype=np.int32))
+    assert eng.is_complete and og.is_complete()
+    assert eng.is_complete_device() == 1
+    eng.compute_all()
+    for s in range(top.n):
+        r = eng.get_row(s)
+        assert np.all(r["flags"] == E.F_DIRECT)
+        for t in range(top.n):
+            lat, rel = og.direct(s, t)
+            assert r["lat"][t] == lat and r["rel"][t] == rel, (s, t)
+    eng.close()
+
+
+def test_multigraph_counted_complete(E, oracle_mod):
+    """_topology_isComplete counts incident EDGES (topology.c:450-552): a
+    complete graph missing edge {a, b} but with a parallel copy of another
+    edge at a and at b still counts as complete, so the reference serves
+    direct paths and (a, b) has none.  The topology mirror matches the
+    oracle's cache protocol on it, query for query."""
+    d = G.dense(40, seed=6)
+    a, b = 3, 17
+    drop = ((d.src == a) & (d.dst == b)) | ((d.src == b) & (d.dst == a))
+    keep = ~drop
+    src = np.concatenate([d.src[keep], [a, b]])
+    dst = np.concatenate([d.dst[keep], [5, 9]])
+    lat_ab = [d.latency[keep][((d.src[keep] == x) & (d.dst[keep] == y)) | ((d.src[keep] == y) & (d.dst[keep] == x))][0]
+              for x, y in ((a, 5), (b, 9))]
+    top = Topology(d.n, False, src, dst, np.concatenate([d.latency[keep], lat_ab]),
+                   np.concatenate([d.loss[keep], [0.01, 0.02]]), d.vloss)
+    og = oracle_mod.OracleGraph(top)
+    att = np.arange(top.n, dtype=np.int32)
+    eng = E.Engine(top, att)
+    assert og.is_complete() and eng.is_complete and eng.is_complete_device() == 1
+    ref = oracle_mod.OracleTopology(og, att)
+    shim = E.TopologyShim(eng)
+    pairs = [(a, b), (b, a), (a, a), (a, 5), (5, a), (b, 9)]
+    rng = np.random.default_rng(2)
+    pairs += [tuple(int(x) for x in rng.integers(0, top.n, 2)) for _ in range(1500)]
+    for s, t in pairs:
+        x = (ref.get_latency(s, t), ref.get_reliability(s, t), ref.is_routable(s, t))
+        y = (shim.get_latency(s, t), shim.get_reliability(s, t), shim.is_routable(s, t))
+        assert x == y, (s, t, x, y)
+    assert ref.cache_size == shim.cache_size
+    shim.close()
+    eng.close()
 
 
 def test_invalid_latency_rejected(E):

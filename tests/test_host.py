@@ -62,6 +62,35 @@ def test_engine_fails_loudly_without_gpu(lib):
     assert ei.value.code == ENODEV
 
 
+def test_multigraph_host_build_without_gpu(lib):
+    """The host graph build runs before the device check: a multigraph whose
+    newest parallel edge is a fastest one of its group is accepted (the create
+    then stops at ENODEV on this GPU-less box), one whose newest parallel edge
+    -- igraph_get_eid's edge, the one the reference folds -- is slower than
+    another is rejected with EMULTI, for edges and for parallel self-loops."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from shdpe.engine import Engine, EngineError, ENODEV, EMULTI
+    from shdpe.graph import Topology
+    base = G.random_sparse(60, 4, seed=2)
+    for directed in (False, True):
+        b = G.random_sparse(60, 4, seed=2, directed=directed)
+        with pytest.raises(EngineError) as ei:
+            Engine(G.with_parallel_edges(b, 0.4, seed=3), np.arange(60))
+        assert ei.value.code == ENODEV
+        with pytest.raises(EngineError) as ei:
+            Engine(G.with_parallel_edges(b, 0.4, seed=3, consistent=False, loops=False), np.arange(60))
+        assert ei.value.code == EMULTI
+    # two self-loops on vertex 0, the newer one slower
+    top = Topology(base.n, False, np.concatenate([base.src, [0]]), np.concatenate([base.dst, [0]]),
+                   np.concatenate([base.latency, [base.latency[base.src == base.dst][0] + 1.0]]),
+                   np.concatenate([base.loss, [0.0]]))
+    with pytest.raises(EngineError) as ei:
+        Engine(top, np.arange(60))
+    assert ei.value.code == EMULTI
+
+
 def test_strerror(lib):
     from shdpe.engine import strerror
     assert "multigraph" in strerror(-6)
