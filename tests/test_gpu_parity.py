@@ -109,6 +109,18 @@ def test_exact_kernel_heap_tail_in_global(E, oracle_mod, monkeypatch):
     assert st["rowsExact"] == 100
 
 
+@pytest.mark.parametrize("n,hc", [(3000, 2100), (20000, 2400)])
+def test_exact_kernel_small_lds_top(E, oracle_mod, monkeypatch, n, hc):
+    """k_exact_rows with a small LDS top of the heap (hc of 2,100 / 2,400
+    positions: most sift-downs, pushes and modifies reach the global tail) on
+    quantised power-law graphs above the all-LDS size: every row bit-exact."""
+    monkeypatch.setenv("SHDPE_EXACT_HC", str(hc))
+    top = G.power_law(n, m=3, seed=21, quantum=0.5)
+    att = G.sample_attached(n, 300, seed=5)
+    st = _check_engine(E, oracle_mod, top, att, sources=att[:24], force=3, debug_flags=E.DEBUG_ENV)
+    assert st["rowsExact"] == 24
+
+
 def test_exact_kernel_large_graph_global_index(E, oracle_mod):
     """n > 24k: index2 in global memory, heap head in LDS, tail in global."""
     top = G.power_law(30_000, m=2, seed=12)
@@ -208,7 +220,7 @@ def test_multigraph_rejected(E):
 
 
 @pytest.mark.parametrize("directed", [False, True], ids=["undirected", "directed"])
-@pytest.mark.parametrize("quantum", [0.0, 5.0], ids=["tiefree", "quantised"])
+@pytest.mark.parametrize("quantum", [0.0, 10.0], ids=["tiefree", "quantised"])
 @pytest.mark.parametrize("force", [0, 5], ids=["sparse", "batched"])
 def test_multigraph_rows(E, oracle_mod, directed, quantum, force):
     """Multigraphs (topology.c:417-420: igraph_get_eid picks the newest parallel
