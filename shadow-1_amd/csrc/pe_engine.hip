@@ -841,7 +841,9 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     int rc;
     // split kernels: one persisted dist array per batch of a round (relax ->
     // post), the rest per resident workgroup; rounds sized by free memory
-    // (at most 96 GiB of dist arrays: C4 one round of 13 GB, C5 two)
+    // (at most 160 GiB of dist arrays: C4 one round of 13 GB, C5 one round
+    // of 131 GB beside its 107 GB table -- 2 rounds under a 96 GiB cap were
+    // 5% slower, profiles/r04_ab_notes.txt r04i)
     size_t roundB = slots;
     if (sh->bcfg.split) {
         size_t freeB = 0, totalB = 0;
@@ -849,7 +851,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
         const size_t perD = NS * LB * 8;
         const size_t rest = slots * (perSlot - NS * LB * 8);
         const size_t room = freeB > rest + ((size_t)12 << 30) ? freeB - rest - ((size_t)12 << 30) : perD;
-        const size_t dBudget = std::min<size_t>(room, (size_t)96 << 30);
+        const size_t dBudget = std::min<size_t>(room, (size_t)160 << 30);
         roundB = std::max<size_t>(slots, std::min<size_t>(nBatchesAll, dBudget / perD));
     }
     sh->batchRound = (int32_t)roundB;

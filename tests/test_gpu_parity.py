@@ -666,17 +666,18 @@ def test_batched_kernel_each_lb(E, oracle_mod, monkeypatch, lb, wpe, case):
         assert st["rowsExact"] > 0
 
 
-@pytest.mark.parametrize("coop,sub", [(2, 0), (4, 0), (1, 1), (2, 1), (4, 2)])
+@pytest.mark.parametrize("coop,sub,lb", [(2, 0, 16), (4, 0, 16), (1, 1, 16), (2, 1, 16), (4, 2, 16),
+                                         (2, 0, 8), (4, 1, 8)])
 @pytest.mark.parametrize("wpe", [4, 8])
 @pytest.mark.parametrize("case", ["power_law", "quantized"])
-def test_batched_cooperative_relax(E, oracle_mod, monkeypatch, coop, sub, wpe, case):
-    """Small shards: the relax kernel with coop workgroups per LB-16 batch
-    (shared dist array and published near bitmaps in uncached memory, a
-    memory-side barrier per phase) and the post kernel over 2^sub lane
+def test_batched_cooperative_relax(E, oracle_mod, monkeypatch, coop, sub, lb, wpe, case):
+    """Small shards: the relax kernel with coop workgroups per LB-16 / LB-8
+    batch (shared dist array and published near bitmaps in uncached memory,
+    a memory-side barrier per phase) and the post kernel over 2^sub lane
     slices of each batch; bit-exact with the oracle, tie rows included."""
     monkeypatch.setenv("SHDPE_BATCH_COOP", str(coop))
     monkeypatch.setenv("SHDPE_BATCH_POST_SUB", str(sub))
-    monkeypatch.setenv("SHDPE_BATCH_LB", "16")
+    monkeypatch.setenv("SHDPE_BATCH_LB", str(lb))
     monkeypatch.setenv("SHDPE_BATCH_WPE", str(wpe))
     if case == "power_law":
         top = G.power_law(8000, m=3, seed=16)
@@ -685,7 +686,7 @@ def test_batched_cooperative_relax(E, oracle_mod, monkeypatch, coop, sub, wpe, c
     else:
         top, att, srcs = G.random_sparse(600, 6, seed=216, quantum=1.0), np.arange(599), None
     st = _check_engine(E, oracle_mod, top, att, sources=srcs, force=5, debug_flags=E.DEBUG_ENV)
-    assert st["batched"] == 1 and st["batchLanes"] == 16 and st["batchWaves"] == wpe
+    assert st["batched"] == 1 and st["batchLanes"] == lb and st["batchWaves"] == wpe
     if case == "quantized":
         assert st["rowsExact"] > 0
 
