@@ -36,6 +36,8 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     int32_t* q = malloc(sizeof(int32_t) * n);
     uint64_t* dirty = calloc(n, 8);
     uint8_t* farp = calloc(n, 1);
+    uint8_t* farp2 = calloc(n, 1);   // farMode & 8: keys beyond the next bucket
+    int farNext = 0;                 // something entered farp (the next bucket) this bucket
     int32_t* stamp = malloc(sizeof(int32_t) * n);
     uint64_t* hpend = calloc(n, 8);   // lanes whose heavy arcs wait for their bucket to settle
     for (int v = 0; v < n; ++v) stamp[v] = -1;
@@ -49,6 +51,8 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
         const double* off = offs + (size_t)b * LB;
         const double* vk = vkey ? vkey + (size_t)b * n : NULL;
 #define KEY(v, l, d) (vk ? vk[v] : (d) - off[l])
+#define FARSET(v, k) do { if ((farMode & 8) && (k) >= bound + delta) farp2[v] = 1; \
+                          else { farp[v] = 1; farNext = 1; } } while (0)
         for (size_t i = 0; i < (size_t)n * LB; ++i) D[i] = INFINITY;
         memset(pend, 0, n);
         memset(dirty, 0, 8 * (size_t)n);
@@ -107,7 +111,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                                 D[(size_t)x * LB + l] = nb;
                                 const double kx = KEY(x, l, nb);
                                 if (kx < bound) nextp[x] = 1;   // cannot happen (w >= delta)
-                                else { farp[x] = 1; if (kx < farMin) farMin = kx; }
+                                else { FARSET(x, kx); if (kx < farMin) farMin = kx; }
                                 dirty[x] |= 1ull << l;
                                 anyImp = 1;
                                 out->laneImp += 1;
@@ -126,8 +130,20 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 closed = bound;
                 for (int v = 0; v < n; ++v) if (recP[v]) { recP[v] = 0; recF[v] = 1; }
                 bound = nb;
-                memcpy(pend, farp, n);
-                memset(farp, 0, n);
+                if (!(farMode & 8)) {
+                    memcpy(pend, farp, n);
+                    memset(farp, 0, n);
+                } else if (farNext) {          // next bucket: near <- F, F <- F2
+                    memcpy(pend, farp, n);
+                    memcpy(farp, farp2, n);
+                    memset(farp2, 0, n);
+                } else {                       // jump: near <- F2
+                    memcpy(pend, farp2, n);
+                    memset(farp, 0, n);
+                    memset(farp2, 0, n);
+                }
+                farNext = 0;
+                if (farMode & 8) for (int v = 0; v < n; ++v) if (farp[v]) { farNext = 1; break; }
                 continue;
             }
             memset(pend, 0, n);
@@ -146,7 +162,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                     const double key = KEY(u, l, du[l]);
                     if (key < bound) act |= 1ull << l;
                     else if (farMode) {
-                        farp[u] = 1;
+                        FARSET(u, key);
                         if (key < farMin) farMin = key;
                     } else {
                         nextp[u] = 1;
@@ -198,7 +214,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                         if (nb < D[(size_t)x * LB + l]) {
                             D[(size_t)x * LB + l] = nb;
                             if (farMode && KEY(x, l, nb) >= bound) {
-                                farp[x] = 1;
+                                FARSET(x, KEY(x, l, nb));
                                 if (KEY(x, l, nb) < farMin) farMin = KEY(x, l, nb);
                             } else {
                                 nextp[x] = 1;
@@ -228,6 +244,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     free(q);
     free(dirty);
     free(farp);
+    free(farp2);
     free(stamp);
     free(hpend);
     free(recP);
