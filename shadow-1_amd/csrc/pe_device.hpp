@@ -81,7 +81,7 @@ struct Tuning {
     int relabel = 1;           // batched path: 1 = device ids by descending degree, 0 = as given
     int batchSplit = 1;        // batched path: relax / post as two kernels (predecessors on demand)
     int batchDUncached = 0;    // batched path: dist arrays in uncached (memory-side coherent) memory
-    int batchCoop = 1;         // batched path: workgroups per batch in the relax kernel (1, 2, 4)
+    int batchCoop = 0;         // batched path: workgroups per batch in the relax kernel (1, 2, 4; 0 = auto)
     int batchPostSub = 0;      // batched path: post-kernel items per batch = 2^batchPostSub
     double batchDeltaFactor = 0.75, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
