@@ -78,6 +78,7 @@ struct Shard {
     int32_t batchRound = 0;         // split kernels: batches per round (persisted dist arrays)
     int32_t batchSlots = 0;         // scratch slots allocated (no launch may exceed it)
     int32_t coopK = 1;              // relax workgroups per batch (cooperative relax)
+    bool sharesDevice = false;      // another shard of this engine runs on the same GPU
     int32_t postSub = 0;            // post items per batch = 2^postSub (lanes split)
     int32_t* dBatchRows = nullptr;
     uint8_t* dBatchAmb = nullptr;
@@ -298,7 +299,10 @@ static int configure(ShdPe* pe, Shard* sh) {
     if (autoLB)
         b.lb = tu.batchCoop > 1 || ((int64_t)sh->rowCount + 15) / 16 >= 2 * (int64_t)sh->numCUs ? 16 : 8;
     sh->coopK = tu.batchCoop == 2 || tu.batchCoop == 4 ? tu.batchCoop : 1;
-    if (tu.batchCoop == 0 && autoLB && b.lb == 8 &&
+    // (not when shards of this engine share the GPU: their concurrent
+    // kernels could keep a group's members from being co-resident, and a
+    // group that cannot meet sends its rows to the exact kernel)
+    if (tu.batchCoop == 0 && autoLB && b.lb == 8 && !sh->sharesDevice &&
         ((int64_t)sh->rowCount + 7) / 8 < 2 * (int64_t)sh->numCUs)
         sh->coopK = 2;
     sh->postSub = std::max(0, std::min(2, tu.batchPostSub));
@@ -726,6 +730,7 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
         sh->rowStart = pe->bounds[sh->gindex];
         sh->rowCount = pe->bounds[sh->gindex + 1] - sh->rowStart;
         sh->fullOwner = std::find(devs.begin(), devs.begin() + i, devs[i]) == devs.begin() + i;
+        sh->sharesDevice = std::count(devs.begin(), devs.begin() + o.nDevices, devs[i]) > 1;
         rc = init_shard(pe.get(), sh.get());
         pe->shards.push_back(std::move(sh));
         if (rc) { shd_pe_destroy(pe.release()); return rc; }
