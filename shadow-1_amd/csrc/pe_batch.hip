@@ -265,8 +265,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const int member = coop ? (int)(blockIdx.x % coopK) : 0;
     const int group = coop ? (int)(blockIdx.x / coopK) : 0;
     const int nGroups = coop ? (int)(gridDim.x / coopK) : 1;
-    uint32_t* pubNear = coop ? bs.pub + (size_t)group * coopK * nwp : nullptr;
-    unsigned long long* pubS = coop ? bs.pubS + (size_t)group * coopK * 2 : nullptr;
+    // two publication buffers per group, alternating by phase: a member that
+    // publishes phase p + 1 while its partner still reads phase p's bits
+    // (nothing to process itself in p) must not overwrite them -- it cannot
+    // reach phase p + 2's buffer before the partner passed the barrier of p + 1
+    uint32_t* pubNear = coop ? bs.pub + (size_t)group * 2 * coopK * nwp : nullptr;
+    unsigned long long* pubS = coop ? bs.pubS + (size_t)group * 2 * coopK * 2 : nullptr;
+    int pp = 0;
     int* bar = coop ? bs.bar + group * 16 : nullptr;
     int epoch = 0, citer = 0;
     // post kernel over sub-batches: 2^subShift items per batch, LB of the
@@ -388,10 +393,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     atomicMin(&ctl->farMin, myFar);
                     myFar = INF_BITS;
                 }
+                pp ^= 1;
+                uint32_t* const pn = pubNear + (size_t)pp * coopK * nwp;
+                unsigned long long* const ps = pubS + (size_t)pp * coopK * 2;
                 int cnt = 0;
                 for (int w = tid; w < nw; w += NT) {
                     const uint32_t bits = anyC.ld(w);
-                    __hip_atomic_store(&pubNear[(size_t)member * nwp + w], bits, __ATOMIC_RELAXED,
+                    __hip_atomic_store(&pn[(size_t)member * nwp + w], bits, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                     if (bits) { anyC.st(w, 0u); cnt += __popc(bits); }
                 }
@@ -399,10 +407,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 fence_wg();
                 __syncthreads();
                 if (tid == 0) {
-                    __hip_atomic_store(&pubS[member * 2], (unsigned long long)ctl->pubCnt |
+                    __hip_atomic_store(&ps[member * 2], (unsigned long long)ctl->pubCnt |
                                        ((unsigned long long)(ctl->farAny != 0) << 32),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&pubS[member * 2 + 1], ctl->farMin, __ATOMIC_RELAXED,
+                    __hip_atomic_store(&ps[member * 2 + 1], ctl->farMin, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                     ctl->pubCnt = 0;
                 }
@@ -411,9 +419,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 int fany = 0;
                 for (int k = 0; k < coopK; ++k) {
                     const unsigned long long a =
-                        __hip_atomic_load(&pubS[k * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_load(&ps[k * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const unsigned long long f =
-                        __hip_atomic_load(&pubS[k * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_load(&ps[k * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     tot += a & 0xFFFFFFFFull;
                     fany |= (int)(a >> 32);
                     fmin = f < fmin ? f : fmin;
@@ -435,7 +443,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 if (coop) {
                     bits = 0u;
                     for (int k = 0; k < coopK; ++k)
-                        bits |= __hip_atomic_load(&pubNear[(size_t)k * nwp + w], __ATOMIC_RELAXED,
+                        bits |= __hip_atomic_load(&pubNear[((size_t)pp * coopK + k) * nwp + w], __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
                 } else {
                     bits = anyC.ld(w);

@@ -907,10 +907,11 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
         // members of a group may sit on different XCDs
         const size_t nwp = (size_t)batch_bits_words(pe->hg.n) / 2;
         void *pub, *pubS, *bar;
-        if (hipExtMallocWithFlags(&pub, slots * nwp * 4, hipDeviceMallocUncached) != hipSuccess)
+        // (two buffers per group, alternating by phase)
+        if (hipExtMallocWithFlags(&pub, 2 * slots * nwp * 4, hipDeviceMallocUncached) != hipSuccess)
             return SHD_PE_ENOMEM;
         sh->allocs.push_back(pub);
-        if (hipExtMallocWithFlags(&pubS, slots * 16, hipDeviceMallocUncached) != hipSuccess)
+        if (hipExtMallocWithFlags(&pubS, 2 * slots * 16, hipDeviceMallocUncached) != hipSuccess)
             return SHD_PE_ENOMEM;
         sh->allocs.push_back(pubS);
         if (hipExtMallocWithFlags(&bar, slots * 64 + 64, hipDeviceMallocUncached) != hipSuccess)
