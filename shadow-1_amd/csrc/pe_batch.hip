@@ -95,9 +95,18 @@ __device__ __forceinline__ void relax_min(unsigned long long* p, unsigned long l
     __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// dist loads of the relax part.  The cooperative relax (`agent`) reads at
+// agent scope, past the CU's L1: a line another member has since changed
+// must not be served stale from this CU's L1 -- a stale DIRTY value of a
+// vertex processed again would be relaxed and marked clean once more, and
+// the newer value its partner wrote (whose near bit was already consumed)
+// would never be relaxed.
+__device__ __forceinline__ unsigned long long ld_dist(unsigned long long* p, bool agent) {
+    return agent ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ld_wg(p);
+}
 // relax pre-check load
-__device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, int x, int LB, int l) {
-    return ld_wg(&D[(size_t)x * LB + l]);
+__device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, int x, int LB, int l, bool agent) {
+    return ld_dist(&D[(size_t)x * LB + l], agent);
 }
 
 __device__ __forceinline__ void mark_clean(unsigned long long* p, unsigned long long e) {
@@ -232,6 +241,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                                            int32_t nBatches, uint8_t* rowAmbig,
                                                            double delta, int32_t* dbg,
                                                            const TieBuf* __restrict__ tieDesc) {
+    // PART 3: the relax kernel of the cooperative relax (PART 1 with coopK
+    // workgroups per batch); a separate instantiation so the plain relax
+    // keeps its own code and register budget
+    constexpr int PT = PART == 3 ? 1 : PART;
     constexpr int BV = BCfg<WPE>::BV;
     constexpr int SMAX = BCfg<WPE>::SMAX;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -260,7 +273,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const size_t NS = (size_t)bs.nStride;
     const size_t SE = NS * LB;
     // cooperative relax: K members per batch (static batch assignment)
-    const int coopK = PART == 1 ? bs.coopK : 1;
+    const int coopK = PART == 3 ? bs.coopK : 1;
     const bool coop = coopK > 1;
     const int member = coop ? (int)(blockIdx.x % coopK) : 0;
     const int group = coop ? (int)(blockIdx.x / coopK) : 0;
@@ -276,7 +289,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     int epoch = 0, citer = 0;
     // post kernel over sub-batches: 2^subShift items per batch, LB of the
     // batch's LB << subShift lanes each (dist arrays keep the full stride)
-    const int subShift = PART == 2 ? bs.subShift : 0;
+    const int subShift = PT == 2 ? bs.subShift : 0;
     const int DLB = LB << subShift;
     unsigned long long* D = as_global(bs.D + slot * SE);
     double* R = as_global(bs.R + slot * SE);
@@ -297,13 +310,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         const int row = batchRows[(size_t)b * DLB + dl];
         const int src = row >= 0 ? g.attached[row] : -1;
         if (gid == 0) laneRow[l] = row;
-        if constexpr (PART != 0) D = as_global(bs.D + (size_t)b * NS * DLB);
+        if constexpr (PT != 0) D = as_global(bs.D + (size_t)b * NS * DLB);
         // ---- init: dist = +inf (clean) for all (v, lane); pending sets empty ----
         {
             ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
             const size_t cnt2 = NE / 2;
             const ulonglong2 inf2 = make_ulonglong2(INF_ENC, INF_ENC);
-            if constexpr (PART != 2) {
+            if constexpr (PT != 2) {
                 const size_t i0 = cnt2 * member / coopK, i1 = cnt2 * (member + 1) / coopK;
                 for (size_t i = i0 + tid; i < i1; i += NT) D2[i] = inf2;
             }
@@ -322,7 +335,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->pubCnt = 0;
             }
         }
-        if (PART == 1 && coop && member == 0 && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 0);
+        if (PT == 1 && coop && member == 0 && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 0);
         fence_wg();
         __syncthreads();
         bool coopOk = true;
@@ -331,7 +344,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // key = dist + (maxOff - off) lines the lanes up behind the hub
         const double off = (row >= 0 && bs.rowOff) ? as_global(bs.rowOff)[row] : 0.0;
         if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
-        if (PART != 2 && gid == 0 && src >= 0) {
+        if (PT != 2 && gid == 0 && src >= 0) {
             if (member == 0) D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
             R[(size_t)src * LB + l] = 1.0;
             any0.set(src);
@@ -363,11 +376,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         long long procs = 0, arcsDone = 0, lanesAct = 0;
         double bound = delta;
         unsigned long long myFar = INF_BITS;      // smallest far key this thread added
-        if constexpr (PART == 2) failed = as_global(bs.flags)[b] != 0;
+        if constexpr (PT == 2) failed = as_global(bs.flags)[b] != 0;
         uint32_t needMask = 0u;
         long long tPh2 = 0;
         for (int attempt = 0;; ++attempt) {
-        const bool fullPred = PART != 2 || attempt > 0;
+        const bool fullPred = PT != 2 || attempt > 0;
         if (attempt > 0) {
             if (tid == 0) {
                 ctl->qtail = 0;
@@ -378,7 +391,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
         }
         for (;;) {   // phases + verification until the Bellman check holds
-        if constexpr (PART != 2) {
+        if constexpr (PT != 2) {
         for (;;) {
             if (failed) break;
             const Bits<GB> anyC = par ? any1 : any0;   // near
@@ -508,7 +521,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 for (int h = wv; h < hn; h += NW) {
                     const int u = ld_wg(&Q[NS - 1 - h]);
                     unsigned long long* const pu = &D[(size_t)u * LB + l];
-                    const unsigned long long e0 = ld_wg(pu);
+                    const unsigned long long e0 = ld_dist(pu, coop);
                     const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
                     const double k0 = b2d(dec(e0)) + sh;
                     const bool dirty = is_dirty(e0);
@@ -544,7 +557,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[k] = relax_ld(D, xs[k] >= 0 ? xs[k] : 0, LB, l);
+                            dx[k] = relax_ld(D, xs[k] >= 0 ? xs[k] : 0, LB, l, coop);
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const int x = xs[k];
@@ -599,7 +612,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 for (int v = 0; v < BV; ++v) {
                     // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
                     const int uc = u[v] >= 0 ? u[v] : 0;
-                    const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                    const unsigned long long d0 = ld_dist(&D[(size_t)uc * LB + l], coop);
                     const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
                     db[v] = u[v] >= 0 ? d0 : INF_ENC;
                     a0[v] = u[v] >= 0 ? r0 : 0;
@@ -652,7 +665,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l);
+                            dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l, coop);
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
@@ -705,9 +718,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             ++phases;
             __syncthreads();
         }
-        }   // PART != 2
+        }   // PT != 2
         if (dbg) tPh1 = (long long)clock64();
-        if constexpr (PART == 1) break;
+        if constexpr (PT == 1) break;
 
         // ================= 2. Bellman check + predecessor pass ===============
         // (a) every entry must satisfy dist[v] <= dist[u] + w for all in-arcs
@@ -876,13 +889,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         }
         __syncthreads();
         if (!anyViol || failed) break;
-        if constexpr (PART == 2) {   // no relaxation here to repair with: exact path
+        if constexpr (PT == 2) {   // no relaxation here to repair with: exact path
             failed = true;
             break;
         }
         ++repairs;
         }   // verification loop
-        if constexpr (PART == 1) {
+        if constexpr (PT == 1) {
             if (coop) {                     // a failed member fails the batch (memory-side)
                 if (failed && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 1);
             } else if (tid == 0) {
@@ -1116,7 +1129,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (!fullPred && !failed && (retry || needMask)) continue;
         break;
         }   // attempts
-        if constexpr (PART == 1) {
+        if constexpr (PT == 1) {
             if (dbg && tid == 0) {
                 dbg[16 * b + 0] = phases;
                 dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
@@ -1188,7 +1201,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             rowAmbig[(size_t)b * DLB + dl] =
                 ((needMask >> l) & 1u) ? (uint8_t)(tieSlot[l] >= 0 ? 2 + tieSlot[l] : 1) : (uint8_t)0;
         if (dbg && tid == 0) {
-            if (PART == 0) {
+            if (PT == 0) {
                 dbg[16 * b + 0] = phases;
                 dbg[16 * b + 15] = repairs;
                 dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
@@ -1245,7 +1258,8 @@ static const void* kptr(int lb, bool gb) {
 
 template <int WPE>
 static const void* kptr_p(int lb, bool gb, int part) {
-    return part == 1 ? kptr<WPE, 1>(lb, gb) : part == 2 ? kptr<WPE, 2>(lb, gb) : kptr<WPE, 0>(lb, gb);
+    return part == 1 ? kptr<WPE, 1>(lb, gb) : part == 2 ? kptr<WPE, 2>(lb, gb)
+         : part == 3 ? kptr<WPE, 3>(lb, gb) : kptr<WPE, 0>(lb, gb);
 }
 
 const void* batch_kernel_ptr(int lb, int wpe, bool gbits, int part) {
@@ -1274,7 +1288,9 @@ static void launch_wp(const DevGraph& g, const DevTable& tab, const BatchScratch
                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid,
                       int part) {
-    if (part == 1) launch_w<WPE, 1>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    if (part == 1 && bs.coopK > 1)
+        launch_w<WPE, 3>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    else if (part == 1) launch_w<WPE, 1>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (part == 2) launch_w<WPE, 2>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else launch_w<WPE, 0>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
 }
