@@ -73,7 +73,14 @@ struct alignas(16) BCtrl {
     unsigned long long busySum;
     double maxOff;    // largest lane offset of the batch (bits via atomicMax)
     int pubCnt;       // cooperative relax: near bits published this phase
+    // SHD_PE_DEBUG_COUNTERS only: vertex processings, arcs, active lanes and
+    // the relax / predecessor phase timestamps (in LDS, not registers: the
+    // relax loop runs at its VGPR cap)
+    unsigned int dProcs, dArcs, dLanes;
+    long long t0, t1, t2;
 };
+static_assert(sizeof(BCtrl) <= 128, "batch control block");
+constexpr int BCTRL_BYTES = 128;
 
 // Entry encoding of the [v][LB] distance array: (f64 bits << 1) | dirty.
 // Positive doubles have bit 63 clear, so the shift loses nothing and the u64
@@ -266,7 +273,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 
     BCtrl* ctl = reinterpret_cast<BCtrl*>(smem);
     uint32_t* const bits0 = GB ? as_global(bs.bits) + (size_t)blockIdx.x * 2 * nwp
-                               : reinterpret_cast<uint32_t*>(smem + 64);
+                               : reinterpret_cast<uint32_t*>(smem + BCTRL_BYTES);
     const Bits<GB> any0{bits0}, any1{bits0 + nwp};
 
     const size_t slot = blockIdx.x;
@@ -333,6 +340,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->busySum = 0;
                 ctl->maxOff = 0.0;
                 ctl->pubCnt = 0;
+                ctl->dProcs = ctl->dArcs = ctl->dLanes = 0u;
             }
         }
         if (PT == 1 && coop && member == 0 && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 0);
@@ -368,17 +376,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // encoding (the line was just read for the pre-check, so the atomic
         // resolves in L2, and no update is lost).  The Bellman check of pass
         // 2 stays as the safety net.
-        const long long tPh0 = dbg ? (long long)clock64() : 0;
-        long long tPh1 = 0;
+        if (dbg && tid == 0) ctl->t0 = (long long)clock64();
         int par = 0, phases = 0, repairs = 0;
         bool failed = !coopOk;
         const int phaseCap = 8 * n + 1024;
-        long long procs = 0, arcsDone = 0, lanesAct = 0;
         double bound = delta;
         unsigned long long myFar = INF_BITS;      // smallest far key this thread added
         if constexpr (PT == 2) failed = as_global(bs.flags)[b] != 0;
         uint32_t needMask = 0u;
-        long long tPh2 = 0;
         for (int attempt = 0;; ++attempt) {
         const bool fullPred = PT != 2 || attempt > 0;
         if (attempt > 0) {
@@ -538,10 +543,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     if (gw == 0 && act) mark_clean(pu, e0);
                     const unsigned long long dub1 = act ? dec(e0) : INF_BITS;
                     if (!__ballot(amask != 0)) continue;       // wave-uniform
-                    if (gw == 0) {
-                        ++procs;
-                        arcsDone += a1 - a0;
-                        lanesAct += __popc(amask);
+                    if (dbg && gw == 0 && l == 0) {
+                        atomicAdd(&ctl->dProcs, 1u);
+                        atomicAdd(&ctl->dArcs, (unsigned int)(a1 - a0));
+                        atomicAdd(&ctl->dLanes, (unsigned int)__popc(amask));
                     }
                     for (int t = a0 + gw * BK; t < a1; t += GPW * BK) {
                         int xs[BK];
@@ -636,10 +641,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     if (act) mark_clean(&D[(size_t)u[v] * LB + l], db[v]);
                     dub[v] = act ? dec(db[v]) : INF_BITS;
                     if (!amask) a1[v] = a0[v];
-                    else {
-                        ++procs;
-                        arcsDone += a1[v] - a0[v];
-                        lanesAct += __popc(amask);
+                    else if (dbg && l == 0) {
+                        atomicAdd(&ctl->dProcs, 1u);
+                        atomicAdd(&ctl->dArcs, (unsigned int)(a1[v] - a0[v]));
+                        atomicAdd(&ctl->dLanes, (unsigned int)__popc(amask));
                     }
                     maxd = max(maxd, a1[v] - a0[v]);
                 }
@@ -719,7 +724,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
         }
         }   // PT != 2
-        if (dbg) tPh1 = (long long)clock64();
+        if (dbg && tid == 0) ctl->t1 = (long long)clock64();
         if constexpr (PT == 1) break;
 
         // ================= 2. Bellman check + predecessor pass ===============
@@ -903,7 +908,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             }
             break;
         }
-        if (dbg) tPh2 = (long long)clock64();
+        if (dbg && tid == 0) ctl->t2 = (long long)clock64();
 
         // ================= 3. labels on demand + row writer ==================
         // Only entries on some target's path need hops and reliability (27%
@@ -928,7 +933,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         for (int pass = 0; pass < 2; ++pass) {
         bool deep = false;
         if (!failed && row >= 0) {
-            int2* const stk = reinterpret_cast<int2*>(smem + 64);
+            int2* const stk = reinterpret_cast<int2*>(smem + BCTRL_BYTES);
             const int T = (int)tab.T;
             // pass 0: the deep-tree budget; pass 1: only the never-spin net
             // (every consistent entry is resolved by then)
@@ -1049,7 +1054,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // the table is never re-read here)
         if (!failed && !retry) {
             const int T = (int)tab.T;
-            double* const tLat = reinterpret_cast<double*>(smem + 64);
+            double* const tLat = reinterpret_cast<double*>(smem + BCTRL_BYTES);
             double* const tRel = tLat + NT;
             int32_t* const tHop = reinterpret_cast<int32_t*>(tRel + NT);
             int32_t* const tPred = tHop + NT;
@@ -1130,15 +1135,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         break;
         }   // attempts
         if constexpr (PT == 1) {
+            __syncthreads();
             if (dbg && tid == 0) {
                 dbg[16 * b + 0] = phases;
-                dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
+                dbg[16 * b + 5] = (int)((ctl->t1 - ctl->t0) >> 10);
                 dbg[16 * b + 15] = repairs;
-            }
-            if (dbg && l == 0 && procs) {
-                atomicAdd(&dbg[16 * b + 4], (int)procs);
-                atomicAdd(&dbg[16 * b + 9], (int)(arcsDone >> 4));
-                atomicAdd(&dbg[16 * b + 10], (int)lanesAct);
+                atomicAdd(&dbg[16 * b + 4], (int)ctl->dProcs);
+                atomicAdd(&dbg[16 * b + 9], (int)(ctl->dArcs >> 4));
+                atomicAdd(&dbg[16 * b + 10], (int)ctl->dLanes);
             }
             __syncthreads();
             continue;
@@ -1204,19 +1208,17 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             if (PT == 0) {
                 dbg[16 * b + 0] = phases;
                 dbg[16 * b + 15] = repairs;
-                dbg[16 * b + 5] = (int)((tPh1 - tPh0) >> 10);
+                dbg[16 * b + 5] = (int)((ctl->t1 - ctl->t0) >> 10);
+                atomicAdd(&dbg[16 * b + 4], (int)ctl->dProcs);
+                atomicAdd(&dbg[16 * b + 9], (int)(ctl->dArcs >> 4));
+                atomicAdd(&dbg[16 * b + 10], (int)ctl->dLanes);
             }
             dbg[16 * b + 1] = 0;
             dbg[16 * b + 2] = 0;
             dbg[16 * b + 3] = (int)needMask;
-            dbg[16 * b + 6] = (int)((tPh2 - tPh1) >> 10);
-            dbg[16 * b + 7] = (int)((tPh3 - tPh2) >> 10);
+            dbg[16 * b + 6] = (int)((ctl->t2 - ctl->t1) >> 10);
+            dbg[16 * b + 7] = (int)((tPh3 - ctl->t2) >> 10);
             dbg[16 * b + 11] = (int)((tPh4 - tPh3) >> 10);
-        }
-        if (dbg && l == 0 && procs) {
-            atomicAdd(&dbg[16 * b + 4], (int)procs);
-            atomicAdd(&dbg[16 * b + 9], (int)(arcsDone >> 4));
-            atomicAdd(&dbg[16 * b + 10], (int)lanesAct);
         }
         fence_wg();
         __syncthreads();
@@ -1242,7 +1244,7 @@ int batch_lds_bytes(int n, int wpe, bool gbits) {
     // label walks reuse the relax bitmaps' LDS for their stacks
     const int stack = batch_threads(wpe) * (wpe >= 6 ? BCfg<8>::SMAX : BCfg<4>::SMAX) * 8;
     const int bits = gbits ? 0 : 2 * 4 * nwp;
-    return 64 + (bits > stack ? bits : stack);
+    return BCTRL_BYTES + (bits > stack ? bits : stack);
 }
 
 int64_t batch_bits_words(int n) { return 2 * (int64_t)((((n + 31) >> 5) + 3) & ~3); }
