@@ -77,7 +77,7 @@ struct alignas(16) BCtrl {
     // the relax / predecessor phase timestamps (in LDS, not registers: the
     // relax loop runs at its VGPR cap)
     unsigned int dProcs, dArcs, dLanes;
-    long long t0, t1, t2;
+    long long t0, t1, t2, t3, t4;
 };
 static_assert(sizeof(BCtrl) <= 128, "batch control block");
 constexpr int BCTRL_BYTES = 128;
@@ -1147,7 +1147,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
             continue;
         }
-        const long long tPh3 = dbg ? (long long)clock64() : 0;
+        if (dbg && tid == 0) ctl->t3 = (long long)clock64();
 
         // ---- tie export: hand k_exact_rows the final distances, the parents
         // and the ambiguous entries, so it emulates the heap only until the
@@ -1198,7 +1198,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             tieSlot[tid] = -1;
         }
         __syncthreads();
-        const long long tPh4 = dbg ? (long long)clock64() : 0;
+        if (dbg && tid == 0) ctl->t4 = (long long)clock64();
         // 0 fast path, 1 full igraph-heap emulation, 2 + slot: early-stop
         // emulation with the exported tie data
         if (gid == 0 && row >= 0)
@@ -1217,12 +1217,12 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             dbg[16 * b + 2] = 0;
             dbg[16 * b + 3] = (int)needMask;
             dbg[16 * b + 6] = (int)((ctl->t2 - ctl->t1) >> 10);
-            dbg[16 * b + 7] = (int)((tPh3 - ctl->t2) >> 10);
-            dbg[16 * b + 11] = (int)((tPh4 - tPh3) >> 10);
+            dbg[16 * b + 7] = (int)((ctl->t3 - ctl->t2) >> 10);
+            dbg[16 * b + 11] = (int)((ctl->t4 - ctl->t3) >> 10);
         }
         fence_wg();
         __syncthreads();
-        if (dbg && tid == 0) dbg[16 * b + 8] = (int)(((long long)clock64() - tPh4) >> 10);
+        if (dbg && tid == 0) dbg[16 * b + 8] = (int)(((long long)clock64() - ctl->t4) >> 10);
     }
 }
 
