@@ -43,7 +43,8 @@
 namespace shdpe {
 
 constexpr int BT_THREADS = 1024;
-constexpr int BK = 4;        // arcs per vertex per load batch
+constexpr int BK = 4;        // arcs per vertex per load batch (relaxation)
+constexpr int BKP = 4;       // in-arcs per vertex per load batch (predecessor pass)
 // WPE = waves per SIMD the kernel is compiled for: 4 (128 VGPRs, one
 // 1024-thread workgroup per CU, two vertices interleaved per group) or 8
 // (64 VGPRs, two workgroups per CU, one vertex per group)
@@ -780,14 +781,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 int maxd = 0;
 #pragma unroll
                 for (int v = 0; v < BV; ++v) maxd = max(maxd, a1[v] - a0[v]);
-                for (int t = 0; t < maxd; t += BK) {
-                    int cu[BV][BK];
-                    double lw[BV][BK];
-                    unsigned long long du[BV][BK];
+                for (int t = 0; t < maxd; t += BKP) {
+                    int cu[BV][BKP];
+                    double lw[BV][BKP];
+                    unsigned long long du[BV][BKP];
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
-                        for (int k = 0; k < BK; ++k) {      // branch-free (see pass 1)
+                        for (int k = 0; k < BKP; ++k) {      // branch-free (see pass 1)
                             const int a = a0[v] + t + k;
                             const bool ok = a < a1[v];
                             const int ac = ok ? a : 0;
@@ -805,7 +806,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
-                        for (int k = 0; k < BK; ++k) {
+                        for (int k = 0; k < BKP; ++k) {
                             const unsigned long long t2 =
                                 dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * DLB + dl]));
                             du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
@@ -813,7 +814,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
-                        for (int k = 0; k < BK; ++k) {
+                        for (int k = 0; k < BKP; ++k) {
                             if (cu[v][k] < 0 || root[v]) continue;
                             const double cand = b2d(du[v][k]) + lw[v][k];
                             const unsigned long long cb = d2b(cand);
