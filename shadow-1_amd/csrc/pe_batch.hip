@@ -43,8 +43,8 @@
 namespace shdpe {
 
 constexpr int BT_THREADS = 1024;
-constexpr int BK = 4;        // arcs per vertex per load batch (relaxation)
-constexpr int BKP = 4;       // in-arcs per vertex per load batch (predecessor pass)
+constexpr int BK = 3;        // arcs per vertex per load batch (relaxation)
+constexpr int BKP = 3;       // in-arcs per vertex per load batch (predecessor pass)
 // WPE = waves per SIMD the kernel is compiled for: 4 (128 VGPRs, one
 // 1024-thread workgroup per CU, two vertices interleaved per group) or 8
 // (64 VGPRs, two workgroups per CU, one vertex per group)
