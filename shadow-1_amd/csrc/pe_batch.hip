@@ -171,6 +171,16 @@ __device__ __forceinline__ double next_bound(double mn, double delta) {
     return nb;
 }
 
+// workgroup-uniform values read from LDS, pinned to scalar registers (the
+// relax loop runs at its VGPR cap)
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ double uni(double x) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 __device__ __forceinline__ void st_wg(int32_t* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -360,7 +370,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         }
         fence_wg();
         __syncthreads();
-        const double sh = ctl->maxOff - off;      // >= 0: keys are non-negative
+        const double sh = uni(ctl->maxOff) - off;      // >= 0: keys are non-negative
 
         // ================= 1. delta-stepping over the batch =================
         // Pending state is one bit per VERTEX (LDS) in two sets: NEAR (some
@@ -495,15 +505,15 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             }
             fence_wg();
             __syncthreads();
-            const int qn = ctl->qtail;
-            const int hn = ctl->htail;
+            const int qn = uni(ctl->qtail);
+            const int hn = uni(ctl->htail);
             if (qn == 0 && hn == 0 && (!coop || !coopNear)) {   // (coop: the group's near set)
                 // bucket settled: advance to the far set, or done
-                const int farAny = ctl->farAny;
-                const double fm = b2d(ctl->farMin);
+                const int farAny = uni(ctl->farAny);
+                const double fm = uni(b2d(ctl->farMin));
                 __syncthreads();
                 if (!farAny) break;
-                bound = fm < b2d(INF_BITS) ? next_bound(fm, delta) : b2d(INF_BITS);
+                bound = uni(fm < b2d(INF_BITS) ? next_bound(fm, delta) : b2d(INF_BITS));
                 if (tid == 0) {
                     ctl->farAny = 0;
                     ctl->farMin = INF_BITS;
@@ -751,7 +761,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 }
                 fence_wg();
                 __syncthreads();
-                hi = ctl->qtail;
+                hi = uni(ctl->qtail);
                 __syncthreads();
             }
             while (lo < hi) {
@@ -876,7 +886,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             fence_wg();
             __syncthreads();
             lo = hi;
-            hi = ctl->qtail;
+            hi = uni(ctl->qtail);
             __syncthreads();
             }
             if (!fullPred) {
@@ -887,7 +897,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (viol) ctl->changed = 1;
         fence_wg();
         __syncthreads();
-        const int anyViol = ctl->changed;
+        const int anyViol = uni(ctl->changed);
         __syncthreads();
         if (tid == 0) {
             ctl->changed = 0;
@@ -1003,7 +1013,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (deep) ctl->changed = 1;
         fence_wg();
         __syncthreads();
-        const int anyDeep = ctl->changed;
+        const int anyDeep = uni(ctl->changed);
         __syncthreads();
         if (tid == 0) ctl->changed = 0;
         __syncthreads();
@@ -1040,7 +1050,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             if (ch) ctl->changed = 1;
             fence_wg();
             __syncthreads();
-            const int any = ctl->changed;
+            const int any = uni(ctl->changed);
             __syncthreads();
             if (tid == 0) ctl->changed = 0;
             __syncthreads();
