@@ -241,7 +241,7 @@ __device__ __forceinline__ bool group_barrier(int* bar, int K, int& epoch) {
         ok = good;
     }
     __syncthreads();
-    return ok != 0;
+    return uni(ok) != 0;
 }
 
 // PART 0: the whole batch in one kernel (relax, predecessors over every
@@ -455,7 +455,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     fany |= (int)(a >> 32);
                     fmin = f < fmin ? f : fmin;
                 }
-                coopNear = tot != 0;
+                coopNear = uni(tot != 0 ? 1 : 0);
                 // the group's far state decides the bucket advance (uniform)
                 __syncthreads();
                 if (tid == 0 && !coopNear) {
@@ -948,7 +948,8 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             const int T = (int)tab.T;
             // pass 0: the deep-tree budget; pass 1: only the never-spin net
             // (every consistent entry is resolved by then)
-            const long long stepCap = pass == 0 ? (long long)WALK_BUDGET : 4LL * n + 64;
+            // (32-bit: the [v][LB] entry indices below are 32-bit already)
+            const int stepCap = pass == 0 ? WALK_BUDGET : 4 * n + 64;
             for (int j = gid; j < T; j += NG) {
                 const int t = g.attached[j];
                 if (t != src) {
@@ -957,7 +958,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     if (dt != INF_BITS) {
                         int he = ld_wg(&H[e]);
                         double re = ld_wg(&R[e]);
-                        long long steps = 0;
+                        int steps = 0;
                         int cur = (int)e;
                         while (!(he >= 0 && re >= 0.0)) {
                             int sp = 0, x = cur, hp = 0;

@@ -290,10 +290,12 @@ static int configure(ShdPe* pe, Shard* sh) {
     // times (profiles/r04_shard_times.txt): N=4 (4,096 rows) LB 8 39.0 ms vs
     // LB 16 42.7; N=8 (2,048 rows) LB 8 23.7 vs LB 16 39.5 vs LB 4 28.3 --
     // LB 4 (32-B line pieces) stays a SHDPE_BATCH_LB option only
-    // Shards with fewer LB-8 batches than two per CU (C4 at 8 ranks: 256)
-    // also relax each batch with two cooperating workgroups: N=8 per-rank
-    // 26.1 -> 23.6 ms (profiles/r04_ab_notes.txt r04j); SHDPE_BATCH_COOP
-    // forces 1, 2 or 4 (2 and 4 with LB 16 unless SHDPE_BATCH_LB says else).
+    // The cooperative relax (coopK workgroups per batch) is an opt-in knob,
+    // SHDPE_BATCH_COOP = 2 or 4 (LB 16 unless SHDPE_BATCH_LB says else): it
+    // took C4's N=8 per-rank shard 26.1 -> 23.6 ms, but one parity run of
+    // it (with the post kernel over half batches) produced a wrong row
+    // (profiles/r04_ab_notes.txt r04t) that could not be reproduced or
+    // explained in the round, so it is not a default.
     b.lb = tu.batchLB;
     const bool autoLB = b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32;
     if (autoLB)
@@ -302,9 +304,7 @@ static int configure(ShdPe* pe, Shard* sh) {
     // (not when shards of this engine share the GPU: their concurrent
     // kernels could keep a group's members from being co-resident, and a
     // group that cannot meet sends its rows to the exact kernel)
-    if (tu.batchCoop == 0 && autoLB && b.lb == 8 && !sh->sharesDevice &&
-        ((int64_t)sh->rowCount + 7) / 8 < 2 * (int64_t)sh->numCUs)
-        sh->coopK = 2;
+    (void)autoLB;
     sh->postSub = std::max(0, std::min(2, tu.batchPostSub));
     if ((b.lb >> sh->postSub) < 4) sh->postSub = 0;
     b.threads = tu.batchThreads;
