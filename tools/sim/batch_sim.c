@@ -22,6 +22,9 @@ typedef struct {
                         // bucket bound (final for all lanes: the D-line read is avoidable)
     double skip2;       // ... and known to be so through a record made when the head was last
                         // processed with all lanes' keys below that phase's bound (2-bitmap scheme)
+    double impv;        // distinct vertices improved per phase, summed over phases
+    double impvMax;     // ... the largest phase
+    double impvOver[4]; // phases with more than 128 / 256 / 512 / 1024 improved vertices
 } SimOut;
 
 // vkey (optional, [nBatch][n]): a per-VERTEX bucket key replacing every
@@ -39,8 +42,9 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     uint8_t* farp2 = calloc(n, 1);   // farMode & 8: keys beyond the next bucket
     int farNext = 0;                 // something entered farp (the next bucket) this bucket
     int32_t* stamp = malloc(sizeof(int32_t) * n);
+    int32_t* istamp = malloc(sizeof(int32_t) * n);   // improved in phase gphase
     uint64_t* hpend = calloc(n, 8);   // lanes whose heavy arcs wait for their bucket to settle
-    for (int v = 0; v < n; ++v) stamp[v] = -1;
+    for (int v = 0; v < n; ++v) stamp[v] = istamp[v] = -1;
     uint8_t* recP = calloc(n, 1);   // all lanes below the bound when last processed (this bucket)
     uint8_t* recF = calloc(n, 1);   // ... in a closed bucket: final
     int32_t gphase = 0;
@@ -150,6 +154,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
             memset(nextp, 0, n);
             ++gphase;
             int active = 0;
+            int impPhase = 0;
             double minNext = INFINITY;
             out->cands += qn;
             for (int i = 0; i < qn; ++i) {
@@ -220,6 +225,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                                 nextp[x] = 1;
                             }
                             dirty[x] |= 1ull << l;
+                            if (istamp[x] != gphase) { istamp[x] = gphase; ++impPhase; }
                             active = 1;
                             anyImp = 1;
                             out->laneImp += 1;
@@ -230,6 +236,9 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
             }
             memcpy(pend, nextp, n);
             out->phases += 1;
+            out->impv += impPhase;
+            if (impPhase > out->impvMax) out->impvMax = impPhase;
+            for (int k = 0; k < 4; ++k) out->impvOver[k] += impPhase > (128 << k);
             if (!active && !farMode) {
                 const double mn = minNext;
                 double nb = (floor(mn / delta) + 1.0) * delta;
@@ -246,6 +255,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     free(farp);
     free(farp2);
     free(stamp);
+    free(istamp);
     free(hpend);
     free(recP);
     free(recF);

@@ -20,7 +20,8 @@ class Out(ctypes.Structure):
     _fields_ = [("procs", ctypes.c_double), ("arcs", ctypes.c_double),
                 ("phases", ctypes.c_double), ("lanesAct", ctypes.c_double), ("cands", ctypes.c_double),
                 ("touched", ctypes.c_double), ("improving", ctypes.c_double), ("laneImp", ctypes.c_double),
-                ("skippable", ctypes.c_double), ("skip2", ctypes.c_double)]
+                ("skippable", ctypes.c_double), ("skip2", ctypes.c_double),
+                ("impv", ctypes.c_double), ("impvMax", ctypes.c_double), ("impvOver", ctypes.c_double * 4)]
 
 
 def lib():
@@ -77,6 +78,7 @@ def run(L, rp, col, w, n, batches, offs, LB, delta, heavy=64, dirty=0, far=0, vk
     run.cands = out.cands / nb / n
     run.extra = (out.touched / nb / col.shape[0], out.improving / nb / col.shape[0], out.laneImp / nb / n / LB)
     run.skip = (out.skippable / max(out.arcs, 1), out.skip2 / max(out.arcs, 1))
+    run.impv = (out.impv / max(out.phases, 1), out.impvMax, [x / max(out.phases, 1) for x in out.impvOver])
     return out.procs / nb / n, out.arcs / nb / col.shape[0], out.phases / nb
 
 
