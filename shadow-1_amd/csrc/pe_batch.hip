@@ -603,9 +603,15 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             }
             // Groups take BV queue entries at a time from an LDS counter, so
             // the phase ends when the last entry is done rather than when the
-            // unluckiest static share is.  The entries of a group's NEXT take
-            // are loaded one iteration ahead, so a vertex starts with its dist
-            // / row-range loads instead of a dependent queue round trip.
+            // unluckiest static share is.  Software-pipelined two takes deep:
+            // while a take relaxes its arcs, the NEXT take's dist lines and
+            // row ranges are in flight and the queue entries of the take
+            // after it -- a vertex starts with its values at hand instead of
+            // two dependent round trips (a listed vertex with no active lane
+            // costs no wait at all).  A value loaded early may be stale;
+            // like any racing read it is only ever larger (entries decrease):
+            // relaxing from it is wasted work, and its clean mark (atomic min)
+            // leaves a newer dirty value dirty for the next listing round.
             const int qc = qn > 0 ? qn - 1 : 0;
             auto take = [&]() {
                 int i = 0;
@@ -613,27 +619,38 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 return __shfl(i, gbase, 64);
             };
             int i0 = take();
+            int u[BV], a0[BV], a1[BV];
+            unsigned long long db[BV];
+#pragma unroll
+            for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? ld_wg(&Q[min(i0 + v, qc)]) : -1;
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
+                const int uc = u[v] >= 0 ? u[v] : 0;
+                const unsigned long long d0 = ld_dist(&D[(size_t)uc * LB + l], coop);
+                const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
+                db[v] = u[v] >= 0 ? d0 : INF_ENC;
+                a0[v] = u[v] >= 0 ? r0 : 0;
+                a1[v] = u[v] >= 0 ? r1 : 0;
+            }
+            int i1 = take();
             int nq[BV];
 #pragma unroll
-            for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i0 + v, qc)]);
+            for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i1 + v, qc)]);
             while (i0 < qn) {
-                int u[BV], a0[BV], a1[BV];
-                unsigned long long db[BV], dub[BV];
-#pragma unroll
-                for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? nq[v] : -1;
-                const int i1 = take();
-#pragma unroll
-                for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i1 + v, qc)]);
+                int un[BV], a0n[BV], a1n[BV];
+                unsigned long long dbn[BV], dub[BV];
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
-                    const int uc = u[v] >= 0 ? u[v] : 0;
-                    const unsigned long long d0 = ld_dist(&D[(size_t)uc * LB + l], coop);
-                    const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
-                    db[v] = u[v] >= 0 ? d0 : INF_ENC;
-                    a0[v] = u[v] >= 0 ? r0 : 0;
-                    a1[v] = u[v] >= 0 ? r1 : 0;
+                    un[v] = i1 + v < qn ? nq[v] : -1;
+                    const int uc = un[v] >= 0 ? un[v] : 0;
+                    dbn[v] = ld_dist(&D[(size_t)uc * LB + l], coop);
+                    a0n[v] = g.rowPtr[uc];
+                    a1n[v] = g.rowPtr[uc + 1];
                 }
+                const int i2 = take();
+#pragma unroll
+                for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i2 + v, qc)]);
                 int maxd = 0;
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
@@ -710,6 +727,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
                 }
                 i0 = i1;
+                i1 = i2;
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    u[v] = un[v];
+                    db[v] = un[v] >= 0 ? dbn[v] : INF_ENC;
+                    a0[v] = un[v] >= 0 ? a0n[v] : 0;
+                    a1[v] = un[v] >= 0 ? a1n[v] : 0;
+                }
             }
             if (dbg && l == 0) {
                 const unsigned long long bz = (unsigned long long)((long long)clock64() - tg0);
@@ -765,23 +790,55 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 __syncthreads();
             }
             while (lo < hi) {
-            for (int v0 = lo + gid * BV; v0 < hi; v0 += NG * BV) {
-                int a0[BV], a1[BV], ba[BV], cnt[BV], bu[BV], vx[BV];
-                unsigned long long dvb[BV], best[BV], mn[BV];
+            // software-pipelined like the relax's light loop: the next
+            // stride's dist lines and in-arc ranges are in flight while this
+            // stride scans its in-arcs, the list entries one stride further
+            const int S = NG * BV;
+            int v0 = lo + gid * BV;
+            int vx[BV], a0[BV], a1[BV], qv[BV];
+            unsigned long long dvb[BV];
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                const int i = v0 + v;
+                vx[v] = i < hi ? (fullPred ? i : ld_wg(&Q[i])) : -1;
+            }
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                const int vc = vx[v] >= 0 ? vx[v] : 0;
+                const unsigned long long d0 = dec(ld_wg(&D[(size_t)vc * DLB + dl]));
+                const int r0 = undirected ? g.rowPtr[vc] : g.inPtr[vc];
+                const int r1 = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
+                dvb[v] = vx[v] >= 0 ? d0 : INF_BITS;
+                a0[v] = vx[v] >= 0 ? r0 : 0;
+                a1[v] = vx[v] >= 0 ? r1 : 0;
+            }
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                const int i = v0 + S + v;
+                qv[v] = fullPred ? i : ld_wg(&Q[min(i, hi - 1)]);
+            }
+            for (; v0 < hi; v0 += S) {
+                int vxn[BV], a0n[BV], a1n[BV];
+                unsigned long long dvn[BV];
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    vxn[v] = v0 + S + v < hi ? qv[v] : -1;
+                    const int vc = vxn[v] >= 0 ? vxn[v] : 0;
+                    dvn[v] = ld_wg(&D[(size_t)vc * DLB + dl]);
+                    a0n[v] = undirected ? g.rowPtr[vc] : g.inPtr[vc];
+                    a1n[v] = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
+                }
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    const int i = v0 + 2 * S + v;
+                    qv[v] = fullPred ? i : ld_wg(&Q[min(i, hi - 1)]);
+                }
+                int ba[BV], cnt[BV], bu[BV];
+                unsigned long long best[BV], mn[BV];
                 bool root[BV];
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    const int vv = v0 + v < hi ? (fullPred ? v0 + v : ld_wg(&Q[v0 + v])) : -1;
-                    vx[v] = vv;
-                    if (vv >= 0) {
-                        dvb[v] = dec(ld_wg(&D[(size_t)vv * DLB + dl]));
-                        a0[v] = undirected ? g.rowPtr[vv] : g.inPtr[vv];
-                        a1[v] = undirected ? g.rowPtr[vv + 1] : g.inPtr[vv + 1];
-                    } else {
-                        dvb[v] = INF_BITS;
-                        a0[v] = a1[v] = 0;
-                    }
-                    root[v] = vv == src || src < 0;
+                    root[v] = vx[v] == src || src < 0;
                     best[v] = INF_BITS;
                     mn[v] = INF_BITS;
                     cnt[v] = 0;
@@ -880,6 +937,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         const int p = vx[v] >= 0 ? bu[v] : -1;
                         wave_append(Q, &ctl->qtail, p >= 0 && !clm.test_set(p), p);
                     }
+                }
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    vx[v] = vxn[v];
+                    dvb[v] = vxn[v] >= 0 ? dec(dvn[v]) : INF_BITS;
+                    a0[v] = vxn[v] >= 0 ? a0n[v] : 0;
+                    a1[v] = vxn[v] >= 0 ? a1n[v] : 0;
                 }
             }
             if (fullPred) break;
