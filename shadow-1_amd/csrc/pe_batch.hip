@@ -265,6 +265,12 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     constexpr int PT = PART == 3 ? 1 : PART;
     constexpr int BV = BCfg<WPE>::BV;
     constexpr int SMAX = BCfg<WPE>::SMAX;
+    // software pipelining of the light-vertex relax loop and the predecessor
+    // pass (next take's loads in flight): in the 8- and 6-wave variants
+    // (one vertex per group); the 4-wave variant (two per group) issues them
+    // at the next take's start (C4 N=8 per-rank shards: 24.5-24.8 ms with
+    // the tune's pipelined pick vs 23.0-23.2 without, r04ze)
+    constexpr bool PIPE = WPE >= 6;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int tieSlot[LB];
     __shared__ int laneRow[LB];           // table row of each lane (-1: pad)
@@ -603,7 +609,8 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             }
             // Groups take BV queue entries at a time from an LDS counter, so
             // the phase ends when the last entry is done rather than when the
-            // unluckiest static share is.  Software-pipelined two takes deep:
+            // unluckiest static share is.  Software-pipelined two takes deep
+            // (PIPE):
             // while a take relaxes its arcs, the NEXT take's dist lines and
             // row ranges are in flight and the queue entries of the take
             // after it -- a vertex starts with its values at hand instead of
@@ -640,14 +647,18 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             while (i0 < qn) {
                 int un[BV], a0n[BV], a1n[BV];
                 unsigned long long dbn[BV], dub[BV];
+                auto fetch_next = [&]() {
 #pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    un[v] = i1 + v < qn ? nq[v] : -1;
-                    const int uc = un[v] >= 0 ? un[v] : 0;
-                    dbn[v] = ld_dist(&D[(size_t)uc * LB + l], coop);
-                    a0n[v] = g.rowPtr[uc];
-                    a1n[v] = g.rowPtr[uc + 1];
-                }
+                    for (int v = 0; v < BV; ++v) {
+                        const int uc = un[v] >= 0 ? un[v] : 0;
+                        dbn[v] = ld_dist(&D[(size_t)uc * LB + l], coop);
+                        a0n[v] = g.rowPtr[uc];
+                        a1n[v] = g.rowPtr[uc + 1];
+                    }
+                };
+#pragma unroll
+                for (int v = 0; v < BV; ++v) un[v] = i1 + v < qn ? nq[v] : -1;
+                if constexpr (PIPE) fetch_next();
                 const int i2 = take();
 #pragma unroll
                 for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i2 + v, qc)]);
@@ -726,6 +737,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             }
                         }
                 }
+                if constexpr (!PIPE) fetch_next();
                 i0 = i1;
                 i1 = i2;
 #pragma unroll
@@ -820,14 +832,18 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             for (; v0 < hi; v0 += S) {
                 int vxn[BV], a0n[BV], a1n[BV];
                 unsigned long long dvn[BV];
+                auto fetch_next = [&]() {
 #pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    vxn[v] = v0 + S + v < hi ? qv[v] : -1;
-                    const int vc = vxn[v] >= 0 ? vxn[v] : 0;
-                    dvn[v] = ld_wg(&D[(size_t)vc * DLB + dl]);
-                    a0n[v] = undirected ? g.rowPtr[vc] : g.inPtr[vc];
-                    a1n[v] = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
-                }
+                    for (int v = 0; v < BV; ++v) {
+                        const int vc = vxn[v] >= 0 ? vxn[v] : 0;
+                        dvn[v] = ld_wg(&D[(size_t)vc * DLB + dl]);
+                        a0n[v] = undirected ? g.rowPtr[vc] : g.inPtr[vc];
+                        a1n[v] = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
+                    }
+                };
+#pragma unroll
+                for (int v = 0; v < BV; ++v) vxn[v] = v0 + S + v < hi ? qv[v] : -1;
+                if constexpr (PIPE) fetch_next();
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
                     const int i = v0 + 2 * S + v;
@@ -938,6 +954,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         wave_append(Q, &ctl->qtail, p >= 0 && !clm.test_set(p), p);
                     }
                 }
+                if constexpr (!PIPE) fetch_next();
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
                     vx[v] = vxn[v];
