@@ -1,6 +1,6 @@
 """Benchmark: path-table construction (source rows/sec), BASELINE.json metric.
 
-python bench.py --gpus N --steps K --warmup W [--workload c4] [--allgather]
+python bench.py --gpus N --steps K --warmup W [--workload c4] [--no-allgather]
 
 A step = one full path-table construction for the workload (all S source
 rows, S = T = attached vertices).  With N ranks (one process per GPU,
@@ -9,9 +9,14 @@ shardIndex = rank, shardCount = N: the engine's shard plan
 (shd_pe_shard_bounds) gives it a contiguous block of rows with an equal
 number of kernel work units, and it computes only those (strong scaling: the
 table is fixed, ranks split it; no exchange on the data path).
---allgather then assembles the whole table on every GPU through the
-engine-owned RCCL communicator (shd_pe_comm_init + shd_pe_gather, all
-fields), timed separately and never part of `value`.
+With N > 1 the whole table is then assembled on every GPU through the
+engine-owned RCCL communicator (shd_pe_comm_init + shd_pe_gather: one
+ncclAllGather per field over xGMI) and VERIFIED: the owners' per-row 64-bit
+fingerprints taken before the exchange must equal every rank's fingerprints
+of its assembled table (shdpe/gather.py).  Timed separately, never part of
+`value`, reported under "allgather"; a mismatch exits non-zero.  One-GPU
+rehearsal (BENCH_REHEARSE_ONE_GPU=1, ranks share cuda:0, RCCL refuses such a
+communicator) moves the rows over gloo + shd_pe_put_rows instead.
 
 Default workload: C4 (BASELINE.json configs[3], the north_star target:
 100k-vertex power-law topology, 16,384 attached sources).  Inputs (graph,
@@ -195,7 +200,7 @@ def main():
                          "process starts the N rank processes itself")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher self-test: every rank prints its rank env as JSON and exits")
-    ap.add_argument("--secondary", default="c3a,c5",
+    ap.add_argument("--secondary", default="c3a,c3b,c5",
                     help="comma list of further configs timed after the headline (rank 0, N=1; "
                          "'' = off): ms_per_step, rows/s and roofline of each")
     ap.add_argument("--host-fill", type=int, default=1,
@@ -204,7 +209,12 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4")
-    ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--allgather", action="store_true", help="(default with --gpus > 1; kept for old scripts)")
+    ap.add_argument("--no-allgather", action="store_true",
+                    help="N > 1: skip the verified table assembly after the timed region")
+    ap.add_argument("--gather-timeout", type=float, default=300.0,
+                    help="seconds before a hung assembly is reported (error in the line) and the "
+                         "ranks exit")
     ap.add_argument("--sub-shards", type=int, default=1,
                     help="row shards per GPU, computed concurrently on their own streams")
     ap.add_argument("--no-cpu", action="store_true")
@@ -308,46 +318,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    gather = None
-    if args.allgather and dist is not None:
-        # engine-owned RCCL communicator: rank 0 makes the id, torch hands it out
-        uid = [Engine.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(uid[0])
-        barrier_sync()
-        g0 = time.perf_counter()
-        eng.gather()
-        barrier_sync()
-        g1 = time.perf_counter()
-        row_bytes = T * (8 + 8 + 4 + 1 + (4 if eng.store_pred else 0))
-        gather = {"ms": (g1 - g0) * 1e3, "bytes_received_per_rank": (T - count) * row_bytes,
-                  "fields": "lat f64, rel f64, hops i32, flags u8" + (", pred i32" if eng.store_pred else ""),
-                  "how": "shd_pe_gather: RCCL broadcast group (per-shard blocks) over xGMI"}
-
-    d2h = None
-    if args.d2h_rows > 0 and count > 0:
-        # PCIe-inclusive: the shard's rows into host buffers after the timed
-        # region, (a) page-locked buffers from shd_pe_host_alloc (DMA lands in
-        # place), (b) fresh pageable numpy arrays (pinned staging + threaded
-        # host copy; includes first-touch page faults)
-        k = min(args.d2h_rows, count)
-        row_bytes = T * (8 + 8 + 4 + 1 + (4 if eng.store_pred else 0))
-        eng.get_rows(start, min(k, 8))
-        pin = eng.pinned_rows(k)
-        eng.get_rows(start, k, out=pin)          # warm (maps the pinned pages on the device)
-        d0 = time.perf_counter()
-        eng.get_rows(start, k, out=pin)
-        dt = time.perf_counter() - d0
-        del pin
-        p0 = time.perf_counter()
-        eng.get_rows(start, k)
-        dtp = time.perf_counter() - p0
-        d2h = {"rows": int(k), "ms_per_row": dt / k * 1e3, "GB/s": k * row_bytes / dt / 1e9,
-               "pageable_GB/s": k * row_bytes / dtp / 1e9,
-               "pcie_inclusive_rows_per_s": 1.0 / (elapsed / args.steps / count + dt / k),
-               "note": "shd_pe_get_rows after the timed region (not in value): GB/s into "
-                       "shd_pe_host_alloc buffers; pageable_GB/s into fresh numpy arrays"}
-
     rows_total = T * args.steps
     value = rows_total / elapsed
     rl = roofline_of(st, n, m_arcs, T, count)
@@ -385,6 +355,68 @@ def main():
         "batch_lanes": st["batchLanes"] or None,
         "batch_post_kernel_waves": st["batchPostWaves"] or None,
     }
+    # ---- N > 1: the shared table assembled on every rank and verified
+    # (untimed, never in `value`); a watchdog reports a hung exchange in the
+    # line instead of leaving the driver without one ----
+    import threading
+    emitted = threading.Lock()
+    done = threading.Event()
+
+    def emit_once(o):
+        if emitted.acquire(blocking=False):
+            emit(json.dumps(o))
+
+    gather_res = None
+    if world > 1 and not args.no_allgather:
+        from shdpe.gather import gather_and_verify
+
+        def on_timeout():
+            if done.is_set():
+                return
+            o = dict(out, allgather={"verified": False, "transport": "rehearse-host" if rehearse else "rccl",
+                                     "error": f"no completion within {args.gather_timeout:.0f} s"})
+            sys.stderr.write(f"bench.py: rank {rank}: table assembly timed out\n")
+            emit_once(o)
+            os._exit(0)     # value stands; the line says the table was not assembled
+        wd = threading.Timer(args.gather_timeout, on_timeout)
+        wd.daemon = True
+        wd.start()
+        row_bytes = T * (8 + 8 + 4 + 1 + (4 if eng.store_pred else 0))
+        try:
+            gather_res = gather_and_verify(eng, dist, rank, world, T, start, count,
+                                           "host" if rehearse else "rccl", barrier_sync,
+                                           reduce_device=None if rehearse else f"cuda:{local}",
+                                           row_bytes=row_bytes)
+        except Exception as e:       # an RCCL / engine error: reported, value stands
+            gather_res = {"verified": False, "transport": "host" if rehearse else "rccl",
+                          "error": f"{type(e).__name__}: {e}"}
+        wd.cancel()
+        gather_res["fields"] = "lat f64, rel f64, hops i32, flags u8" + (", pred i32" if eng.store_pred else "")
+        out["allgather"] = gather_res
+    d2h = None
+    if args.d2h_rows > 0 and count > 0:
+        # PCIe-inclusive: the shard's rows into host buffers after the timed
+        # region, (a) page-locked buffers from shd_pe_host_alloc (DMA lands in
+        # place), (b) fresh pageable numpy arrays (pinned staging + threaded
+        # host copy; includes first-touch page faults)
+        k = min(args.d2h_rows, count)
+        row_bytes = T * (8 + 8 + 4 + 1 + (4 if eng.store_pred else 0))
+        eng.get_rows(start, min(k, 8))
+        pin = eng.pinned_rows(k)
+        eng.get_rows(start, k, out=pin)          # warm (maps the pinned pages on the device)
+        d0 = time.perf_counter()
+        eng.get_rows(start, k, out=pin)
+        dt = time.perf_counter() - d0
+        del pin
+        p0 = time.perf_counter()
+        eng.get_rows(start, k)
+        dtp = time.perf_counter() - p0
+        d2h = {"rows": int(k), "ms_per_row": dt / k * 1e3, "GB/s": k * row_bytes / dt / 1e9,
+               "pageable_GB/s": k * row_bytes / dtp / 1e9,
+               "pcie_inclusive_rows_per_s": 1.0 / (elapsed / args.steps / count + dt / k),
+               "note": "shd_pe_get_rows after the timed region (not in value): GB/s into "
+                       "shd_pe_host_alloc buffers; pageable_GB/s into fresh numpy arrays"}
+
     if rank == 0 and not args.no_stream:
         sbw = eng.stream_bandwidth()     # 16-B streaming copy kernel, same device
         out["roofline"]["stream_GBps"] = sbw
@@ -398,8 +430,6 @@ def main():
                 out["roofline"]["traffic_GBps"] = tb / (avg_launch_ms * 1e-3) / 1e9
                 out["roofline"]["traffic_frac_of_stream"] = out["roofline"]["traffic_GBps"] / sbw
                 out["roofline"]["traffic_over_algorithmic"] = tb / bytes_per_launch
-    if gather:
-        out["allgather"] = gather
     if d2h:
         out["d2h"] = d2h
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -416,10 +446,15 @@ def main():
         out["secondary"] = [secondary(wl, args.steps, dbg) for wl in args.secondary.split(",") if wl]
     if rank == 0 and world == 1 and args.tie_stress:
         out["tie_stress"] = [tie_stress(wl, args.steps, dbg) for wl in args.tie_stress.split(",") if wl]
-    emit(json.dumps(out))
+    done.set()
+    emit_once(out)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if gather_res is not None and gather_res.get("mismatched_rows_max_over_ranks", 0) > 0:
+        sys.stderr.write(f"bench.py: rank {rank}: assembled table differs from the owners' rows: "
+                         f"{json.dumps(gather_res)}\n")
+        sys.exit(4)
 
 
 def secondary(workload, steps, dbg):

@@ -140,6 +140,9 @@ typedef struct ShdPeStats {
                                   split kernels, the relaxation kernel's          */
     int32_t batchPostWaves;    /* split kernels: the post kernel's variant (the
                                   tune times relax and post separately)           */
+    int64_t rowsTieRepaired;   /* early-stop tie rows whose exported slot failed the
+                                  exact kernel's distance cross-check and were
+                                  recomputed by the full emulation (0 when correct) */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */
@@ -256,6 +259,23 @@ int shd_pe_gather(ShdPe* pe);
  * every process, each calls shd_pe_comm_init. */
 int shd_pe_comm_unique_id(void* out, int32_t bytes);   /* bytes >= 128 */
 int shd_pe_comm_init(ShdPe* pe, const void* uniqueId, int32_t bytes);
+/* Host-transport assembly, the alternative to shd_pe_gather where RCCL has no
+ * communicator (several ranks on one GPU, a host-only channel between nodes):
+ * rows [start, start+count) of ANOTHER engine's shard, received in host
+ * buffers (T entries per row, attached order; pred needed iff storePred), are
+ * written into this engine's full table.  Multi-process engines only
+ * (shardCount > 1, nDevices == 1); own rows -> SHD_PE_EINVAL.  Once every
+ * foreign row has arrived, all rows read from the full table as after
+ * shd_pe_gather. */
+int shd_pe_put_rows(ShdPe* pe, int32_t start, int32_t count, const double* lat, const double* rel,
+                    const int32_t* hops, const int32_t* pred, const uint8_t* flags);
+/* 64-bit fingerprint of each table row [start, start+count) (computed on the
+ * device; own rows, or any row after a gather / put_rows): the wrapping sum
+ * over entries j and fields f (lat, rel, hops, flags, pred if stored) of
+ * splitmix64(bits ^ (j * 0x9e3779b97f4a7c15 + f * 0xd1b54a32d192ed03)), f =
+ * 1..5.  Owners fingerprint their rows before an exchange and every rank the
+ * assembled table after it.  No reference counterpart. */
+int shd_pe_row_checksums(ShdPe* pe, int32_t start, int32_t count, uint64_t* out);
 
 /* Wait for outstanding device work of this engine. */
 int shd_pe_synchronize(ShdPe* pe);

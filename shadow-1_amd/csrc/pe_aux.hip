@@ -206,3 +206,53 @@ void launch_incident_min(const DevGraph& g, const int32_t* dEdgeCount, int32_t* 
 }
 
 }  // namespace shdpe
+
+namespace shdpe {
+
+// ---------------------------------------------------------------------------
+// Row checksums (multi-GPU verification, no reference counterpart): a 64-bit
+// fingerprint per table row, the wrapping sum over its entries j and fields f
+// of splitmix64(bits(f, j) ^ (j * K + c_f)) -- order-free over j so a
+// workgroup reduces it in any order, position-keyed so swapped entries or
+// rows change it.  Owners fingerprint their rows before an exchange, every
+// rank fingerprints the assembled table after it (bench.py; a numpy twin in
+// shdpe/engine.py pins the formula on the CPU).  One 256-thread workgroup per
+// row: a coalesced streaming read of the row's 25-29 B per entry.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+constexpr uint64_t CK_K = 0x9e3779b97f4a7c15ull, CK_C = 0xd1b54a32d192ed03ull;
+
+__global__ __launch_bounds__(256) void k_row_checksums(DevTable tab0, int64_t firstLocal,
+                                                       uint64_t* __restrict__ out) {
+    const DevTable tab = global_view(tab0);
+    __shared__ uint64_t part[4];
+    const int64_t T = tab.T;
+    const size_t base = (size_t)(firstLocal + blockIdx.x) * (size_t)T;
+    uint64_t h = 0;
+    for (int64_t j = threadIdx.x; j < T; j += 256) {
+        const uint64_t kj = (uint64_t)j * CK_K;
+        const size_t o = base + (size_t)j;
+        h += mix64((uint64_t)__double_as_longlong(__builtin_nontemporal_load(&tab.lat[o])) ^ (kj + CK_C));
+        h += mix64((uint64_t)__double_as_longlong(__builtin_nontemporal_load(&tab.rel[o])) ^ (kj + 2 * CK_C));
+        h += mix64((uint64_t)(uint32_t)__builtin_nontemporal_load(&tab.hops[o]) ^ (kj + 3 * CK_C));
+        h += mix64((uint64_t)__builtin_nontemporal_load(&tab.flags[o]) ^ (kj + 4 * CK_C));
+        if (tab.pred) h += mix64((uint64_t)(uint32_t)__builtin_nontemporal_load(&tab.pred[o]) ^ (kj + 5 * CK_C));
+    }
+    for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+void launch_row_checksums(const DevTable& tab, int64_t firstLocal, int32_t rows, uint64_t* dOut,
+                          void* stream) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_row_checksums, dim3(rows), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       tab, firstLocal, dOut);
+}
+
+}  // namespace shdpe

@@ -73,7 +73,6 @@ struct alignas(16) BCtrl {
     unsigned long long busyMax;
     unsigned long long busySum;
     double maxOff;    // largest lane offset of the batch (bits via atomicMax)
-    int pubCnt;       // cooperative relax: near bits published this phase
     // SHD_PE_DEBUG_COUNTERS only: vertex processings, arcs, active lanes and
     // the relax / predecessor phase timestamps (in LDS, not registers: the
     // relax loop runs at its VGPR cap)
@@ -103,18 +102,9 @@ __device__ __forceinline__ void relax_min(unsigned long long* p, unsigned long l
     __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// dist loads of the relax part.  The cooperative relax (`agent`) reads at
-// agent scope, past the CU's L1: a line another member has since changed
-// must not be served stale from this CU's L1 -- a stale DIRTY value of a
-// vertex processed again would be relaxed and marked clean once more, and
-// the newer value its partner wrote (whose near bit was already consumed)
-// would never be relaxed.
-__device__ __forceinline__ unsigned long long ld_dist(unsigned long long* p, bool agent) {
-    return agent ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ld_wg(p);
-}
 // relax pre-check load
-__device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, int x, int LB, int l, bool agent) {
-    return ld_dist(&D[(size_t)x * LB + l], agent);
+__device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, int x, int LB, int l) {
+    return ld_wg(&D[(size_t)x * LB + l]);
 }
 
 __device__ __forceinline__ void mark_clean(unsigned long long* p, unsigned long long e) {
@@ -216,34 +206,6 @@ __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
     return acc;
 }
 
-// Cooperative relax (PART 1, bs.coopK > 1): K workgroups share one batch.
-// Their shared state lives in uncached memory (memory-side coherent across
-// XCDs): the dist array (atomics and loads), each member's published near
-// bitmap and scalars.  group_barrier: every wave drains its memory
-// operations, one lane adds to the group's counter (memory-side atomic) and
-// polls it until all K members arrived for this epoch.  A poll that runs
-// past the spin limit (members not co-resident: never with the engine's
-// occupancy-sized grid) gives up and reports failure instead of hanging.
-__device__ __forceinline__ bool group_barrier(int* bar, int K, int& epoch) {
-    __shared__ int ok;
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    ++epoch;
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int target = epoch * K;
-        int good = 1;
-        for (long long spin = 0;; ++spin) {
-            if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-            if (spin > (1ll << 20)) { good = 0; break; }   // ~1 s
-            __builtin_amdgcn_s_sleep(2);
-        }
-        ok = good;
-    }
-    __syncthreads();
-    return uni(ok) != 0;
-}
-
 // PART 0: the whole batch in one kernel (relax, predecessors over every
 // vertex, labels + writer, tie export).  PART 1 / 2: the same split in two
 // kernels over a round of batches whose dist arrays persist in HBM between
@@ -259,10 +221,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                                            int32_t nBatches, uint8_t* rowAmbig,
                                                            double delta, int32_t* dbg,
                                                            const TieBuf* __restrict__ tieDesc) {
-    // PART 3: the relax kernel of the cooperative relax (PART 1 with coopK
-    // workgroups per batch); a separate instantiation so the plain relax
-    // keeps its own code and register budget
-    constexpr int PT = PART == 3 ? 1 : PART;
+    constexpr int PT = PART;
     constexpr int BV = BCfg<WPE>::BV;
     constexpr int SMAX = BCfg<WPE>::SMAX;
     // software pipelining of the light-vertex relax loop and the predecessor
@@ -296,25 +255,6 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const size_t slot = blockIdx.x;
     const size_t NS = (size_t)bs.nStride;
     const size_t SE = NS * LB;
-    // cooperative relax: K members per batch (static batch assignment)
-    const int coopK = PART == 3 ? bs.coopK : 1;
-    const bool coop = coopK > 1;
-    const int member = coop ? (int)(blockIdx.x % coopK) : 0;
-    const int group = coop ? (int)(blockIdx.x / coopK) : 0;
-    const int nGroups = coop ? (int)(gridDim.x / coopK) : 1;
-    // two publication buffers per group, alternating by phase: a member that
-    // publishes phase p + 1 while its partner still reads phase p's bits
-    // (nothing to process itself in p) must not overwrite them -- it cannot
-    // reach phase p + 2's buffer before the partner passed the barrier of p + 1
-    uint32_t* pubNear = coop ? bs.pub + (size_t)group * 2 * coopK * nwp : nullptr;
-    unsigned long long* pubS = coop ? bs.pubS + (size_t)group * 2 * coopK * 2 : nullptr;
-    int pp = 0;
-    int* bar = coop ? bs.bar + group * 16 : nullptr;
-    int epoch = 0, citer = 0;
-    // post kernel over sub-batches: 2^subShift items per batch, LB of the
-    // batch's LB << subShift lanes each (dist arrays keep the full stride)
-    const int subShift = PT == 2 ? bs.subShift : 0;
-    const int DLB = LB << subShift;
     unsigned long long* D = as_global(bs.D + slot * SE);
     double* R = as_global(bs.R + slot * SE);
     int32_t* H = as_global(bs.H + slot * SE);
@@ -325,25 +265,21 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     // by ~20%, and a workgroup finishing early takes the next one)
     __shared__ int nextB;
     for (;;) {
-        if (tid == 0) nextB = coop ? group + (citer++) * nGroups : atomicAdd(bs.next, 1);
+        if (tid == 0) nextB = atomicAdd(bs.next, 1);
         __syncthreads();
-        const int item = nextB;
-        if (item >= (nBatches << subShift)) break;
-        const int b = item >> subShift;
-        const int dl = ((item & ((1 << subShift) - 1)) * LB) + l;   // lane within the batch
-        const int row = batchRows[(size_t)b * DLB + dl];
+        const int b = nextB;
+        if (b >= nBatches) break;
+        const int row = batchRows[(size_t)b * LB + l];
         const int src = row >= 0 ? g.attached[row] : -1;
         if (gid == 0) laneRow[l] = row;
-        if constexpr (PT != 0) D = as_global(bs.D + (size_t)b * NS * DLB);
+        if constexpr (PT != 0) D = as_global(bs.D + (size_t)b * SE);
         // ---- init: dist = +inf (clean) for all (v, lane); pending sets empty ----
         {
             ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
             const size_t cnt2 = NE / 2;
             const ulonglong2 inf2 = make_ulonglong2(INF_ENC, INF_ENC);
-            if constexpr (PT != 2) {
-                const size_t i0 = cnt2 * member / coopK, i1 = cnt2 * (member + 1) / coopK;
-                for (size_t i = i0 + tid; i < i1; i += NT) D2[i] = inf2;
-            }
+            if constexpr (PT != 2)
+                for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
             for (int w = tid; w < nwp; w += NT) { any0.st(w, 0u); any1.st(w, 0u); }
             if (tid == 0) {
                 ctl->qtail = 0;
@@ -356,21 +292,17 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->busyMax = 0;
                 ctl->busySum = 0;
                 ctl->maxOff = 0.0;
-                ctl->pubCnt = 0;
                 ctl->dProcs = ctl->dArcs = ctl->dLanes = 0u;
             }
         }
-        if (PT == 1 && coop && member == 0 && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 0);
         fence_wg();
         __syncthreads();
-        bool coopOk = true;
-        if (coop) coopOk = group_barrier(bar, coopK, epoch);   // every member's slice is +inf
         // lane offset: the source's distance to its nearest hub (host plan);
         // key = dist + (maxOff - off) lines the lanes up behind the hub
         const double off = (row >= 0 && bs.rowOff) ? as_global(bs.rowOff)[row] : 0.0;
         if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
         if (PT != 2 && gid == 0 && src >= 0) {
-            if (member == 0) D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
+            D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
             R[(size_t)src * LB + l] = 1.0;
             any0.set(src);
         }
@@ -395,7 +327,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // 2 stays as the safety net.
         if (dbg && tid == 0) ctl->t0 = (long long)clock64();
         int par = 0, phases = 0, repairs = 0;
-        bool failed = !coopOk;
+        bool failed = false;
         const int phaseCap = 8 * n + 1024;
         double bound = delta;
         unsigned long long myFar = INF_BITS;      // smallest far key this thread added
@@ -418,73 +350,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             if (failed) break;
             const Bits<GB> anyC = par ? any1 : any0;   // near
             const Bits<GB> anyF = par ? any0 : any1;   // far
-            int coopNear = 1;
-            if (coop) {
-                // publish this member's near bits (set by its relaxations,
-                // for any vertex) and its far scalars; after the barrier a
-                // member lists the merged near bits of the words it owns
-                // (w % K == member: hubs -- the lowest device ids -- spread)
-                if (myFar != INF_BITS) {
-                    atomicMin(&ctl->farMin, myFar);
-                    myFar = INF_BITS;
-                }
-                pp ^= 1;
-                uint32_t* const pn = pubNear + (size_t)pp * coopK * nwp;
-                unsigned long long* const ps = pubS + (size_t)pp * coopK * 2;
-                int cnt = 0;
-                for (int w = tid; w < nw; w += NT) {
-                    const uint32_t bits = anyC.ld(w);
-                    __hip_atomic_store(&pn[(size_t)member * nwp + w], bits, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    if (bits) { anyC.st(w, 0u); cnt += __popc(bits); }
-                }
-                if (cnt) atomicAdd(&ctl->pubCnt, cnt);
-                fence_wg();
-                __syncthreads();
-                if (tid == 0) {
-                    __hip_atomic_store(&ps[member * 2], (unsigned long long)ctl->pubCnt |
-                                       ((unsigned long long)(ctl->farAny != 0) << 32),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&ps[member * 2 + 1], ctl->farMin, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    ctl->pubCnt = 0;
-                }
-                if (!group_barrier(bar, coopK, epoch)) { failed = true; break; }
-                unsigned long long tot = 0, fmin = INF_BITS;
-                int fany = 0;
-                for (int k = 0; k < coopK; ++k) {
-                    const unsigned long long a =
-                        __hip_atomic_load(&ps[k * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const unsigned long long f =
-                        __hip_atomic_load(&ps[k * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    tot += a & 0xFFFFFFFFull;
-                    fany |= (int)(a >> 32);
-                    fmin = f < fmin ? f : fmin;
-                }
-                coopNear = uni(tot != 0 ? 1 : 0);
-                // the group's far state decides the bucket advance (uniform)
-                __syncthreads();
-                if (tid == 0 && !coopNear) {
-                    ctl->farAny = fany;
-                    ctl->farMin = fmin;
-                }
-            }
             // candidates = vertices with a near bit (consumed)
             // (hubs -- degree >= the engine's heavy threshold -- go to a list
             // of their own, processed by whole waves: one 16-lane group on a
             // hub's ~1000 arcs would set the phase's length)
-            for (int w = coop ? member + tid * coopK : tid; coopNear && w < nw; w += coop ? NT * coopK : NT) {
-                uint32_t bits;
-                if (coop) {
-                    bits = 0u;
-                    for (int k = 0; k < coopK; ++k)
-                        bits |= __hip_atomic_load(&pubNear[((size_t)pp * coopK + k) * nwp + w], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    bits = anyC.ld(w);
-                }
+            for (int w = tid; w < nw; w += NT) {
+                uint32_t bits = anyC.ld(w);
                 if (bits) {
-                    if (!coop) anyC.st(w, 0u);
+                    anyC.st(w, 0u);
                     uint32_t hv = bits & g.heavyBits[w];
                     bits &= ~hv;
                     if (bits) {
@@ -513,7 +386,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
             const int qn = uni(ctl->qtail);
             const int hn = uni(ctl->htail);
-            if (qn == 0 && hn == 0 && (!coop || !coopNear)) {   // (coop: the group's near set)
+            if (qn == 0 && hn == 0) {
                 // bucket settled: advance to the far set, or done
                 const int farAny = uni(ctl->farAny);
                 const double fm = uni(b2d(ctl->farMin));
@@ -543,7 +416,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 for (int h = wv; h < hn; h += NW) {
                     const int u = ld_wg(&Q[NS - 1 - h]);
                     unsigned long long* const pu = &D[(size_t)u * LB + l];
-                    const unsigned long long e0 = ld_dist(pu, coop);
+                    const unsigned long long e0 = ld_wg(pu);
                     const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
                     const double k0 = b2d(dec(e0)) + sh;
                     const bool dirty = is_dirty(e0);
@@ -579,7 +452,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[k] = relax_ld(D, xs[k] >= 0 ? xs[k] : 0, LB, l, coop);
+                            dx[k] = relax_ld(D, xs[k] >= 0 ? xs[k] : 0, LB, l);
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const int x = xs[k];
@@ -634,7 +507,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             for (int v = 0; v < BV; ++v) {
                 // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
                 const int uc = u[v] >= 0 ? u[v] : 0;
-                const unsigned long long d0 = ld_dist(&D[(size_t)uc * LB + l], coop);
+                const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
                 const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
                 db[v] = u[v] >= 0 ? d0 : INF_ENC;
                 a0[v] = u[v] >= 0 ? r0 : 0;
@@ -651,7 +524,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                     for (int v = 0; v < BV; ++v) {
                         const int uc = un[v] >= 0 ? un[v] : 0;
-                        dbn[v] = ld_dist(&D[(size_t)uc * LB + l], coop);
+                        dbn[v] = ld_wg(&D[(size_t)uc * LB + l]);
                         a0n[v] = g.rowPtr[uc];
                         a1n[v] = g.rowPtr[uc + 1];
                     }
@@ -709,7 +582,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l, coop);
+                            dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l);
 #pragma unroll
                     for (int v = 0; v < BV; ++v)
 #pragma unroll
@@ -817,7 +690,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
             for (int v = 0; v < BV; ++v) {
                 const int vc = vx[v] >= 0 ? vx[v] : 0;
-                const unsigned long long d0 = dec(ld_wg(&D[(size_t)vc * DLB + dl]));
+                const unsigned long long d0 = dec(ld_wg(&D[(size_t)vc * LB + l]));
                 const int r0 = undirected ? g.rowPtr[vc] : g.inPtr[vc];
                 const int r1 = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
                 dvb[v] = vx[v] >= 0 ? d0 : INF_BITS;
@@ -836,7 +709,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                     for (int v = 0; v < BV; ++v) {
                         const int vc = vxn[v] >= 0 ? vxn[v] : 0;
-                        dvn[v] = ld_wg(&D[(size_t)vc * DLB + dl]);
+                        dvn[v] = ld_wg(&D[(size_t)vc * LB + l]);
                         a0n[v] = undirected ? g.rowPtr[vc] : g.inPtr[vc];
                         a1n[v] = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
                     }
@@ -891,7 +764,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                         for (int k = 0; k < BKP; ++k) {
                             const unsigned long long t2 =
-                                dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * DLB + dl]));
+                                dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]));
                             du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
                         }
 #pragma unroll
@@ -921,7 +794,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const size_t e = (size_t)vv * LB + l;
                     const bool bad = !root[v] && mn[v] < dvb[v];
                     if (bad) {
-                        D[(size_t)vv * DLB + dl] = enc_dirty(mn[v]);
+                        D[(size_t)vv * LB + l] = enc_dirty(mn[v]);
                         viol = 1;
                     }
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
@@ -993,11 +866,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         ++repairs;
         }   // verification loop
         if constexpr (PT == 1) {
-            if (coop) {                     // a failed member fails the batch (memory-side)
-                if (failed && tid == 0) (void)atomicExch(&as_global(bs.flags)[b], 1);
-            } else if (tid == 0) {
-                as_global(bs.flags)[b] = failed ? 1 : 0;
-            }
+            if (tid == 0) as_global(bs.flags)[b] = failed ? 1 : 0;
             break;
         }
         if (dbg && tid == 0) ctl->t2 = (long long)clock64();
@@ -1035,7 +904,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 const int t = g.attached[j];
                 if (t != src) {
                     const size_t e = (size_t)t * LB + l;
-                    const unsigned long long dt = dec(ld_wg(&D[(size_t)t * DLB + dl]));
+                    const unsigned long long dt = dec(ld_wg(&D[(size_t)t * LB + l]));
                     if (dt != INF_BITS) {
                         int he = ld_wg(&H[e]);
                         double re = ld_wg(&R[e]);
@@ -1175,7 +1044,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
                     } else {
                         const size_t e = (size_t)t * LB + l;
-                        const unsigned long long dt = dec(ld_wg(&D[(size_t)t * DLB + dl]));
+                        const unsigned long long dt = dec(ld_wg(&D[(size_t)t * LB + l]));
                         if (dt == INF_BITS) {
                             f |= F_UNREACHABLE;
                         } else {
@@ -1267,17 +1136,17 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 const int pe = ld_wg(&P[e]);
                 const bool am = pe >= 0 && (pe & TIE_AMB);
                 const size_t o = (size_t)sl * (size_t)tie.n + v;
-                tie.D[o] = b2d(dec(ld_wg(&D[(size_t)v * DLB + dl])));
+                tie.D[o] = b2d(dec(ld_wg(&D[(size_t)v * LB + l])));
                 tie.P[o] = pe;
                 if (am) {   // rare: re-derive the tied (minimum tight) predecessor distance
-                    const unsigned long long dv = dec(ld_wg(&D[(size_t)v * DLB + dl]));
+                    const unsigned long long dv = dec(ld_wg(&D[(size_t)v * LB + l]));
                     const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];
                     const int a1 = undirected ? g.rowPtr[v + 1] : g.inPtr[v + 1];
                     unsigned long long mt = INF_BITS;
                     for (int a = a0; a < a1; ++a) {
                         const int u = undirected ? g.col[a] : g.inCol[a];
                         const double w = undirected ? g.lat[a] : g.inLat[a];
-                        const unsigned long long du = dec(ld_wg(&D[(size_t)u * DLB + dl]));
+                        const unsigned long long du = dec(ld_wg(&D[(size_t)u * LB + l]));
                         if (du <= dv && d2b(b2d(du) + w) == dv && du < mt) mt = du;
                     }
                     if (mt != INF_BITS) thr = mt > thr ? mt : thr;
@@ -1295,7 +1164,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // 0 fast path, 1 full igraph-heap emulation, 2 + slot: early-stop
         // emulation with the exported tie data
         if (gid == 0 && row >= 0)
-            rowAmbig[(size_t)b * DLB + dl] =
+            rowAmbig[(size_t)b * LB + l] =
                 ((needMask >> l) & 1u) ? (uint8_t)(tieSlot[l] >= 0 ? 2 + tieSlot[l] : 1) : (uint8_t)0;
         if (dbg && tid == 0) {
             if (PT == 0) {
@@ -1353,8 +1222,7 @@ static const void* kptr(int lb, bool gb) {
 
 template <int WPE>
 static const void* kptr_p(int lb, bool gb, int part) {
-    return part == 1 ? kptr<WPE, 1>(lb, gb) : part == 2 ? kptr<WPE, 2>(lb, gb)
-         : part == 3 ? kptr<WPE, 3>(lb, gb) : kptr<WPE, 0>(lb, gb);
+    return part == 1 ? kptr<WPE, 1>(lb, gb) : part == 2 ? kptr<WPE, 2>(lb, gb) : kptr<WPE, 0>(lb, gb);
 }
 
 const void* batch_kernel_ptr(int lb, int wpe, bool gbits, int part) {
@@ -1383,9 +1251,7 @@ static void launch_wp(const DevGraph& g, const DevTable& tab, const BatchScratch
                       const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                       const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid,
                       int part) {
-    if (part == 1 && bs.coopK > 1)
-        launch_w<WPE, 3>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
-    else if (part == 1) launch_w<WPE, 1>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    if (part == 1) launch_w<WPE, 1>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else if (part == 2) launch_w<WPE, 2>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
     else launch_w<WPE, 0>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
 }
@@ -1394,14 +1260,7 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
                        const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
                        const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream, int part) {
     if (nBatches <= 0) return;
-    int grid;
-    if (part == 1 && bs.coopK > 1) {          // groups of coopK consecutive workgroups
-        const int groups = nBatches < cfg.grid / bs.coopK ? nBatches : cfg.grid / bs.coopK;
-        grid = groups * bs.coopK;
-    } else {
-        const int items = part == 2 ? nBatches << bs.subShift : nBatches;
-        grid = items < cfg.grid ? items : cfg.grid;
-    }
+    const int grid = nBatches < cfg.grid ? nBatches : cfg.grid;
     if (grid <= 0) return;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (cfg.wpe >= 8)

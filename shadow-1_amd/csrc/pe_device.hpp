@@ -80,13 +80,12 @@ struct Tuning {
     int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 1, batchWpe = 0;
     int relabel = 1;           // batched path: 1 = device ids by descending degree, 0 = as given
     int batchSplit = 1;        // batched path: relax / post as two kernels (predecessors on demand)
-    int batchDUncached = 0;    // batched path: dist arrays in uncached (memory-side coherent) memory
-    int batchCoop = 0;         // batched path: workgroups per batch in the relax kernel (1, 2, 4; 0 = auto)
-    int batchPostSub = 0;      // batched path: post-kernel items per batch = 2^batchPostSub
     double batchDeltaFactor = 0.75, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
     int debug = 0, streamWgPerCU = 16;
+    int tieCorrupt = 0;        // tests only: scale one early-stop slot's exported distances
+                               // after the relevance scan (exercises the tie-slot repair)
 };
 
 struct DevScratch {
@@ -118,15 +117,6 @@ struct BatchScratch {
     int32_t* flags;          // split kernels: per batch of the round, 1 = phase cap hit
     const double* rowOff;    // [T] per table position: the source's distance to its
                              // batch hub (bucket key offset; null = no offsets)
-    // cooperative relax (small shards): coopK workgroups per batch, batches
-    // assigned statically to groups of coopK consecutive workgroups; shared
-    // state in uncached memory (the dist arrays too)
-    int32_t coopK;           // 1 = off (relax launches only)
-    uint32_t* pub;           // [group][member][words] published near bitmaps
-    unsigned long long* pubS;   // [group][member][2] near count | farAny << 32, farMin
-    int32_t* bar;            // [group * 16] barrier counters (zeroed per launch)
-    // post kernel: 2^subShift work items per batch of LB << subShift lanes
-    int32_t subShift;
 };
 
 struct BatchLaunch {
@@ -235,6 +225,9 @@ void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, 
 void launch_pairs(const DevGraph& g, const int32_t* dSrc, const int32_t* dDst, int64_t count,
                   int mode, double* dLat, double* dRel, uint8_t* dFlags, void* stream);
 void launch_incident_min(const DevGraph& g, const int32_t* dEdgeCount, int32_t* dOut, void* stream);
+// 64-bit fingerprint per table row (local rows firstLocal .. + rows), pe_aux.hip
+void launch_row_checksums(const DevTable& tab, int64_t firstLocal, int32_t rows, uint64_t* dOut,
+                          void* stream);
 // dense path (pe_dense.hip)
 void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int64_t nArcs,
                         void* stream);

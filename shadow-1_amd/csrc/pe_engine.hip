@@ -77,9 +77,6 @@ struct Shard {
     bool batchReady = false;
     int32_t batchRound = 0;         // split kernels: batches per round (persisted dist arrays)
     int32_t batchSlots = 0;         // scratch slots allocated (no launch may exceed it)
-    int32_t coopK = 1;              // relax workgroups per batch (cooperative relax)
-    bool sharesDevice = false;      // another shard of this engine runs on the same GPU
-    int32_t postSub = 0;            // post items per batch = 2^postSub (lanes split)
     int32_t* dBatchRows = nullptr;
     uint8_t* dBatchAmb = nullptr;
     TieBuf tie{};                   // early-stop tie rows (batched path)
@@ -118,6 +115,8 @@ struct ShdPe {
     std::vector<std::unique_ptr<Shard>> shards;
     std::unique_ptr<std::atomic<uint8_t>[]> rowDone;
     bool gathered = false;
+    int64_t putRows = 0;             // rows imported by shd_pe_put_rows (host transport)
+    bool putInit = false;            // own shard rows copied into the full table
     ncclComm_t xcomm = nullptr;      // cross-process communicator (shd_pe_comm_init)
     int32_t ownStart = 0, ownEnd = 0;
     unsigned char* stage[2] = {nullptr, nullptr};   // pinned host staging (portable)
@@ -171,9 +170,6 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_BATCH_WPE", t.batchWpe);
     gi("SHDPE_RELABEL", t.relabel);
     gi("SHDPE_BATCH_SPLIT", t.batchSplit);
-    gi("SHDPE_BATCH_D_UNCACHED", t.batchDUncached);
-    gi("SHDPE_BATCH_COOP", t.batchCoop);
-    gi("SHDPE_BATCH_POST_SUB", t.batchPostSub);
     gd("SHDPE_BATCH_DELTA_FACTOR", t.batchDeltaFactor);
     gd("SHDPE_BATCH_SCRATCH_GB", t.batchScratchGB);
     gd("SHDPE_DENSE_MIN", t.denseMin);
@@ -182,6 +178,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_DENSE_EPOCHS", t.denseEpochs);
     gi("SHDPE_DEBUG", t.debug);
     gi("SHDPE_STREAM_WG_PER_CU", t.streamWgPerCU);
+    gi("SHDPE_TIE_CORRUPT", t.tieCorrupt);
 }
 
 extern "C" void shd_pe_default_options(ShdPeOptions* opt) {
@@ -289,30 +286,18 @@ static int configure(ShdPe* pe, Shard* sh) {
     // every resident workgroup (two per CU) a batch of 16.  C4 per-rank shard
     // times (profiles/r04_shard_times.txt): N=4 (4,096 rows) LB 8 39.0 ms vs
     // LB 16 42.7; N=8 (2,048 rows) LB 8 23.7 vs LB 16 39.5 vs LB 4 28.3 --
-    // LB 4 (32-B line pieces) stays a SHDPE_BATCH_LB option only
-    // The cooperative relax (coopK workgroups per batch) is an opt-in knob,
-    // SHDPE_BATCH_COOP = 2 or 4 (LB 16 unless SHDPE_BATCH_LB says else): it
-    // took C4's N=8 per-rank shard 26.1 -> 23.6 ms, but one parity run of
-    // it (with the post kernel over half batches) produced a wrong row
-    // (profiles/r04_ab_notes.txt r04t) that could not be reproduced or
-    // explained in the round, so it is not a default.
+    // LB 4 (32-B line pieces) stays a SHDPE_BATCH_LB option only.  (The
+    // round-4 cooperative relax -- K workgroups per batch -- and the post
+    // kernel over lane slices are patches under tools/variants/)
     b.lb = tu.batchLB;
-    const bool autoLB = b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32;
-    if (autoLB)
-        b.lb = tu.batchCoop > 1 || ((int64_t)sh->rowCount + 15) / 16 >= 2 * (int64_t)sh->numCUs ? 16 : 8;
-    sh->coopK = tu.batchCoop == 2 || tu.batchCoop == 4 ? tu.batchCoop : 1;
-    // (not when shards of this engine share the GPU: their concurrent
-    // kernels could keep a group's members from being co-resident, and a
-    // group that cannot meet sends its rows to the exact kernel)
-    (void)autoLB;
-    sh->postSub = std::max(0, std::min(2, tu.batchPostSub));
-    if ((b.lb >> sh->postSub) < 4) sh->postSub = 0;
+    if (b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32)
+        b.lb = ((int64_t)sh->rowCount + 15) / 16 >= 2 * (int64_t)sh->numCUs ? 16 : 8;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
     // control block, else in each slot's global scratch (gbits, LB 16)
     b.gbits = pe->batched && batch_lds_bytes((int)n, 8, false) > LDS ? 1 : 0;
-    if (b.gbits) { b.lb = 16; sh->coopK = 1; }   // the cooperative relax keeps its bitmaps in LDS
+    if (b.gbits) b.lb = 16;
     auto occupancy = [&](int wpe, int threads) {
         const int lds = batch_lds_bytes((int)n, wpe, b.gbits != 0);
         int per = 0;
@@ -730,7 +715,6 @@ extern "C" int shd_pe_create(const ShdPeGraphDesc* graph, const int32_t* attache
         sh->rowStart = pe->bounds[sh->gindex];
         sh->rowCount = pe->bounds[sh->gindex + 1] - sh->rowStart;
         sh->fullOwner = std::find(devs.begin(), devs.begin() + i, devs[i]) == devs.begin() + i;
-        sh->sharesDevice = std::count(devs.begin(), devs.begin() + o.nDevices, devs[i]) > 1;
         rc = init_shard(pe.get(), sh.get());
         pe->shards.push_back(std::move(sh));
         if (rc) { shd_pe_destroy(pe.release()); return rc; }
@@ -844,10 +828,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
     const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
     const size_t grid = (size_t)std::max({sh->bcfg.grid, sh->bcfgAlt.grid, sh->bcfgAlt2.grid});
-    // workgroups that can hold a slot: coopK per batch in the relax kernel,
-    // 2^postSub per batch in the post kernel
-    const size_t items = std::max<size_t>({1, nBatchesAll * (size_t)sh->coopK, nBatchesAll << sh->postSub});
-    const size_t slots = std::min<size_t>({grid, maxSlots, items});
+    const size_t slots = std::min<size_t>({grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
     sh->bcfg.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfg.grid);
     if (sh->bcfgAlt.grid > 0) sh->bcfgAlt.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt.grid);
     if (sh->bcfgAlt2.grid > 0) sh->bcfgAlt2.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt2.grid);
@@ -870,14 +851,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     sh->batchRound = (int32_t)roundB;
     sh->batchSlots = (int32_t)slots;
     void *D, *R, *H, *P, *q, *rows, *amb, *fl;
-    if (pe->tu.batchDUncached || sh->coopK > 1) {   // memory-side coherent dist arrays
-        if (hipExtMallocWithFlags(&D, roundB * NS * LB * 8, hipDeviceMallocUncached) != hipSuccess)
-            return SHD_PE_ENOMEM;
-        sh->allocs.push_back(D);
-    } else if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8))) {
-        return rc;
-    }
-    if ((rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
+    if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
         (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
         (rc = dev_alloc(sh, &q, slots * NS * 4 + 64)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
@@ -896,30 +870,6 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
         void* bits;
         if ((rc = dev_alloc(sh, &bits, slots * bitBytes))) return rc;
         sh->bsc.bits = (uint32_t*)bits;
-    }
-    sh->bsc.coopK = 1;
-    sh->bsc.subShift = 0;
-    sh->bsc.pub = nullptr;
-    sh->bsc.pubS = nullptr;
-    sh->bsc.bar = nullptr;
-    if (sh->coopK > 1) {
-        // published bitmaps / scalars / barrier counters, uncached: the
-        // members of a group may sit on different XCDs
-        const size_t nwp = (size_t)batch_bits_words(pe->hg.n) / 2;
-        void *pub, *pubS, *bar;
-        // (two buffers per group, alternating by phase)
-        if (hipExtMallocWithFlags(&pub, 2 * slots * nwp * 4, hipDeviceMallocUncached) != hipSuccess)
-            return SHD_PE_ENOMEM;
-        sh->allocs.push_back(pub);
-        if (hipExtMallocWithFlags(&pubS, 2 * slots * 16, hipDeviceMallocUncached) != hipSuccess)
-            return SHD_PE_ENOMEM;
-        sh->allocs.push_back(pubS);
-        if (hipExtMallocWithFlags(&bar, slots * 64 + 64, hipDeviceMallocUncached) != hipSuccess)
-            return SHD_PE_ENOMEM;
-        sh->allocs.push_back(bar);
-        sh->bsc.pub = (uint32_t*)pub;
-        sh->bsc.pubS = (unsigned long long*)pubS;
-        sh->bsc.bar = (int32_t*)bar;
     }
     sh->bsc.rowOff = nullptr;
     if (!pe->rowOff.empty()) {
@@ -1040,6 +990,26 @@ static void print_exact_debug(Shard* sh, const std::vector<int32_t>& rows, int32
     }
 }
 
+// SHDPE_TIE_CORRUPT (tests): after the relevance scan, halve the exported
+// distances of the first early-stop slot that still needs the emulation --
+// what a slot filled from another source's distance array would hold.  The
+// exact kernel's consistency check must catch it (rowsTieRepaired).
+static void corrupt_tie_slot(ShdPe* pe, Shard* sh, const std::vector<int32_t>& slots, int32_t nTie) {
+    std::vector<double> thr((size_t)sh->tie.cap), d((size_t)pe->hg.n);
+    if (hipStreamSynchronize(sh->stream) != hipSuccess ||
+        hipMemcpy(thr.data(), sh->tie.thr, thr.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    for (int32_t i = 0; i < nTie; ++i) {
+        const int sl = slots[i];
+        if (!(thr[(size_t)sl] > 0.0)) continue;
+        double* dd = sh->tie.D + (size_t)sl * (size_t)sh->tie.n;
+        if (hipMemcpy(d.data(), dd, d.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+        for (double& x : d) x *= 0.5;
+        (void)hipMemcpy(dd, d.data(), d.size() * 8, hipMemcpyHostToDevice);
+        return;
+    }
+}
+
 // Compute the given table positions (all owned by `sh`), chunked.
 static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count) {
     if (count <= 0) return SHD_PE_OK;
@@ -1142,19 +1112,13 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 // (the post kernel may run another variant: bcfgPost)
                 BatchLaunch post = sh->bcfgPost.grid > 0 ? sh->bcfgPost : sh->bcfg;
                 post.grid = std::min(post.grid, sh->batchSlots);
-                post.lb >>= sh->postSub;            // lanes per post workgroup
                 for (int32_t r0 = 0; r0 < nB; r0 += sh->batchRound) {
                     const int32_t rn = std::min(sh->batchRound, nB - r0);
                     const size_t ro = (size_t)r0 * LB;
                     if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[0], sh->stream));
                     for (int part = 1; part <= 2; ++part) {
                         HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
-                        BatchScratch bs = sh->bsc;
-                        bs.coopK = part == 1 ? sh->coopK : 1;
-                        bs.subShift = part == 2 ? sh->postSub : 0;
-                        if (bs.coopK > 1)
-                            HIPCHK(hipMemsetAsync(bs.bar, 0, (size_t)sh->batchSlots * 64 + 64, sh->stream));
-                        launch_batch_rows(sh->dg, sh->tab, bs, sh->dBatchRows + ro, rn,
+                        launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows + ro, rn,
                                           sh->dBatchAmb + ro, part == 1 ? relax : post,
                                           sh->dDbg ? sh->dDbg + 16 * r0 : nullptr, sh->dTie, sh->stream, part);
                         if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[part], sh->stream));
@@ -1266,6 +1230,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 return rc;
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             if (nTie > 0) launch_tie_scan(sh->dg, sh->dRows, sh->dSlots, nTie, sh->tie, sh->stream);
+            if (nTie > 0 && pe->tu.tieCorrupt) corrupt_tie_slot(pe, sh, exactSlots, nTie);
             if (dense)      // ~n arcs per pop: the workgroup-wide scan
                 launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
                                    sh->exactGrid, sh->exactHc, sh->dXList, sh->stream);
@@ -1283,6 +1248,28 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             HIPCHK(hipEventSynchronize(sh->evB));
             st.msExactKernel += elapsed(sh->evA, sh->evB);
             st.launchesExact++;
+            // early-stop rows whose slot failed the exact kernel's consistency
+            // check (thr = NaN: the exported distances are not this row's):
+            // k_tie_write skipped them; the full emulation recomputes them
+            if (nTie > 0) {
+                std::vector<double> thr((size_t)sh->tie.cap);
+                HIPCHK(hipMemcpy(thr.data(), sh->tie.thr, thr.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<int32_t> redo;
+                for (int32_t i = 0; i < nTie; ++i)
+                    if (std::isnan(thr[(size_t)exactSlots[i]])) redo.push_back(exactRows[i]);
+                if (!redo.empty()) {
+                    std::fprintf(stderr, "[shdpe] shard %d: %zu early-stop tie row(s) failed the slot "
+                                 "consistency check; recomputed by the full emulation\n",
+                                 sh->gindex, redo.size());
+                    HIPCHK(hipMemcpyAsync(sh->dRows, redo.data(), redo.size() * 4, hipMemcpyHostToDevice,
+                                          sh->stream));
+                    launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)redo.size(), sh->exactGrid,
+                                      sh->exactHc, pe->tu.exactHc > 0, nullptr, sh->tie, nullptr, sh->stream);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(hipStreamSynchronize(sh->stream));
+                    st.rowsTieRepaired += (int64_t)redo.size();
+                }
+            }
             if (sh->dXdbg && pe->hg.n > 10240) print_exact_debug(sh, exactRows, nTie);
             st.rowsExact += (int64_t)exactRows.size();
         }
@@ -1736,6 +1723,31 @@ extern "C" int shd_pe_copy_rows_device(ShdPe* pe, int32_t start, int32_t count, 
     return SHD_PE_OK;
 }
 
+extern "C" int shd_pe_row_checksums(ShdPe* pe, int32_t start, int32_t count, uint64_t* out) {
+    if (!pe || !out || start < 0 || count < 0 || (int64_t)start + count > (int64_t)pe->attached.size())
+        return SHD_PE_EINVAL;
+    if (count == 0) return SHD_PE_OK;
+    int rc = ensure_rows(pe, start, count);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(pe->copyMu);
+    std::vector<Piece> pieces;
+    if ((rc = table_pieces(pe, start, count, pieces))) return rc;
+    for (const Piece& pc : pieces) {
+        HIPCHK(hipSetDevice(pc.device));
+        uint64_t* d = nullptr;
+        if (hipMalloc(&d, (size_t)pc.count * 8) != hipSuccess) return SHD_PE_ENOMEM;
+        launch_row_checksums(*pc.tab, (int64_t)pc.start - pc.tab->rowStart, pc.count, d, pc.stream);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out + (pc.start - start), d, (size_t)pc.count * 8, hipMemcpyDeviceToHost,
+                               pc.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(pc.stream);
+        (void)hipFree(d);
+        if (e != hipSuccess) return SHD_PE_EHIP;
+    }
+    return SHD_PE_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Gather: the whole table on every device of this engine (and, with a
 // cross-process communicator, of every engine).
@@ -1814,19 +1826,32 @@ static int gather_locked(ShdPe* pe) {
     if (pe->G == 1) {
         // nothing to exchange
     } else if (pe->xcomm) {
-        // cross-process: every process owns one shard (nDevices == 1); the
-        // group of per-shard broadcasts is an all-gather with shard-sized
-        // blocks landing in place (rows are contiguous per shard)
+        // cross-process: every process owns one shard (nDevices == 1), rows
+        // contiguous per shard.  Equal blocks (the plan's usual outcome, e.g.
+        // C4 over 8 ranks: 2,048 rows each): one ncclAllGather per field
+        // straight into the full table; otherwise a group of per-shard
+        // broadcasts (an all-gather-v with blocks landing in place)
         Shard* s = s0;
+        bool equal = true;
+        for (int g = 1; g < pe->G; ++g)
+            equal = equal && pe->bounds[g + 1] - pe->bounds[g] == pe->bounds[1] - pe->bounds[0];
         if (ncclGroupStart() != ncclSuccess) return SHD_PE_ECOMM;
-        for (int g = 0; g < pe->G && rc == SHD_PE_OK; ++g) {
-            const size_t r0 = (size_t)pe->bounds[g], nr = (size_t)(pe->bounds[g + 1] - pe->bounds[g]);
-            if (!nr) continue;
-            for (const Field& f : fields) {
-                char* dst = (char*)field_ptr(s->full, f) + r0 * ts * f.esize;
-                const void* src = g == s->gindex ? field_ptr(s->tab, f) : (const void*)dst;
-                if (ncclBroadcast(src, dst, nr * ts, f.type, g, pe->xcomm, s->stream) != ncclSuccess)
+        if (equal) {
+            const size_t nr = (size_t)(pe->bounds[1] - pe->bounds[0]);
+            for (const Field& f : fields)
+                if (nr && ncclAllGather(field_ptr(s->tab, f), field_ptr(s->full, f), nr * ts, f.type, pe->xcomm,
+                                        s->stream) != ncclSuccess)
                     rc = SHD_PE_ECOMM;
+        } else {
+            for (int g = 0; g < pe->G && rc == SHD_PE_OK; ++g) {
+                const size_t r0 = (size_t)pe->bounds[g], nr = (size_t)(pe->bounds[g + 1] - pe->bounds[g]);
+                if (!nr) continue;
+                for (const Field& f : fields) {
+                    char* dst = (char*)field_ptr(s->full, f) + r0 * ts * f.esize;
+                    const void* src = g == s->gindex ? field_ptr(s->tab, f) : (const void*)dst;
+                    if (ncclBroadcast(src, dst, nr * ts, f.type, g, pe->xcomm, s->stream) != ncclSuccess)
+                        rc = SHD_PE_ECOMM;
+                }
             }
         }
         if (ncclGroupEnd() != ncclSuccess) rc = SHD_PE_ECOMM;
@@ -1879,6 +1904,60 @@ static int gather_locked(ShdPe* pe) {
     pe->msGather += elapsed(e0, e1);
     for (int32_t p = 0; p < T; ++p) pe->rowDone[p].store(1, std::memory_order_release);
     pe->gathered = true;
+    return SHD_PE_OK;
+}
+
+// Host-transport assembly (no RCCL): rows of other engines' shards arrive in
+// host buffers (MPI, sockets, torch.distributed/gloo -- e.g. several ranks
+// sharing one GPU, where RCCL refuses a communicator) and are written into
+// the full table on every device of this engine; this engine's own rows are
+// copied in on the first call.  Once all T rows are present the engine reads
+// every row from the full table, as after shd_pe_gather.
+extern "C" int shd_pe_put_rows(ShdPe* pe, int32_t start, int32_t count, const double* lat,
+                               const double* rel, const int32_t* hops, const int32_t* pred,
+                               const uint8_t* flags) {
+    if (!pe || start < 0 || count < 0 || (int64_t)start + count > (int64_t)pe->attached.size())
+        return SHD_PE_EINVAL;
+    if (!lat || !rel || !hops || !flags || (pe->opt.storePred && !pred)) return SHD_PE_EINVAL;
+    if (pe->opt.shardCount < 2 || pe->opt.nDevices != 1) return SHD_PE_EINVAL;
+    if (start < pe->ownEnd && start + count > pe->ownStart) return SHD_PE_EINVAL;   // own rows
+    if (count == 0) return SHD_PE_OK;
+    std::lock_guard<std::mutex> lk(pe->mu);
+    std::lock_guard<std::mutex> lk2(pe->copyMu);
+    Shard* s = pe->shards[0].get();
+    int rc = ensure_table(pe, s);
+    if (rc) return rc;
+    if (!pe->putInit) {
+        std::vector<int32_t> all;
+        for (int32_t p = pe->ownStart; p < pe->ownEnd; ++p)
+            if (!row_done(pe, p)) all.push_back(p);
+        if ((rc = compute_positions_locked(pe, all.data(), (int32_t)all.size()))) return rc;
+        if ((rc = ensure_full(pe, s, s))) return rc;
+        HIPCHK(hipSetDevice(s->device));
+        std::vector<Field> fields;
+        table_fields(pe, fields);
+        const size_t ts = pe->attached.size();
+        for (const Field& f : fields)
+            HIPCHK(hipMemcpyAsync((char*)field_ptr(s->full, f) + (size_t)s->rowStart * ts * f.esize,
+                                  field_ptr(s->tab, f), (size_t)s->rowCount * ts * f.esize,
+                                  hipMemcpyDeviceToDevice, s->stream));
+        HIPCHK(hipStreamSynchronize(s->stream));
+        pe->putInit = true;
+    }
+    HIPCHK(hipSetDevice(s->device));
+    const size_t ts = pe->attached.size(), o = (size_t)start * ts, cells = (size_t)count * ts;
+    HIPCHK(hipMemcpyAsync(s->full.lat + o, lat, cells * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->full.rel + o, rel, cells * 8, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->full.hops + o, hops, cells * 4, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipMemcpyAsync(s->full.flags + o, flags, cells, hipMemcpyHostToDevice, s->stream));
+    if (pe->opt.storePred)
+        HIPCHK(hipMemcpyAsync(s->full.pred + o, pred, cells * 4, hipMemcpyHostToDevice, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    pe->putRows += count;
+    if (pe->putRows + (pe->ownEnd - pe->ownStart) >= (int64_t)ts) {
+        for (size_t p = 0; p < ts; ++p) pe->rowDone[p].store(1, std::memory_order_release);
+        pe->gathered = true;
+    }
     return SHD_PE_OK;
 }
 
@@ -2078,6 +2157,7 @@ extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
         t.rowsComputed += s.rowsComputed;
         t.rowsExact += s.rowsExact;
         t.rowsTieEarly += s.rowsTieEarly;
+        t.rowsTieRepaired += s.rowsTieRepaired;
         t.arcsRelaxed += s.arcsRelaxed;
         t.msSparseKernel += s.msSparseKernel;
         t.msExactKernel += s.msExactKernel;

@@ -919,16 +919,33 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
 // pop never improves its distance strictly).  Unmarked entries have a single
 // candidate parent, which the emulation would pick too.  tie_finalize merges
 // the two parent sets; k_tie_write derives hops / reliability along them.
+//
+// Consistency check (round 5): every vertex the emulation popped has its
+// final igraph distance in Dem, which must equal the exported distance of the
+// same row bit for bit.  A slot holding another source's (or a stale)
+// distance array fails it: thr := NaN, k_tie_write leaves the row alone and
+// the engine recomputes it with the full emulation (ShdPeStats.rowsTieRepaired,
+// zero in every correct run).
 // ---------------------------------------------------------------------------
-template <class Reached>
+template <class Reached, class Popped>
 __device__ __forceinline__ void tie_finalize(const TieBuf& tie, int slot, int n, int lane,
-                                             Reached reached, const int32_t* P) {
+                                             Reached reached, Popped popped, const double* Dem,
+                                             const int32_t* P) {
     int32_t* tp = tie.P + (size_t)slot * (size_t)tie.n;
+    const double* td = tie.D + (size_t)slot * (size_t)tie.n;
+    bool bad = false;
     for (int v = lane; v < n; v += EX_THREADS) {
         const int fp = tp[v];
         if (fp >= 0 && (fp & TIE_AMB))
             tp[v] = reached(v) ? P[v] : -1;   // unreached: off every target's path
+        if (popped(v) && d2b(Dem[v]) != d2b(td[v])) bad = true;
     }
+    if (__ballot(bad) && lane == 0) tie.thr[slot] = __longlong_as_double(0x7ff8000000000000ll);
+}
+
+__device__ __forceinline__ bool tie_slot_bad(const TieBuf& tie, int slot) {
+    const double t = tie.thr[slot];
+    return t != t;
 }
 
 // One workgroup per tie row: is any ambiguous entry on the path to a target?
@@ -989,6 +1006,7 @@ __global__ __launch_bounds__(TW_THREADS) void k_tie_write(DevGraph g0, DevTable 
     const int tid = threadIdx.x;
     const int r = rows[blockIdx.x];
     const int s = g.attached[r];
+    if (tie_slot_bad(tie, slots[blockIdx.x])) return;   // the engine recomputes the row
     const size_t off = (size_t)slots[blockIdx.x] * (size_t)tie.n;
     const double* D = tie.D + off;
     const int32_t* P = tie.P + off;
@@ -1363,8 +1381,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
         }
         __syncthreads();
         if (tslot >= 0)
-            tie_finalize(tie, tslot, n, lane,
-                         [&](int v) { return thr >= 0.0 && h.I2[v] != 0; }, P);
+            tie_finalize(tie, tslot, n, lane, [&](int v) { return thr >= 0.0 && h.I2[v] != 0; },
+                         [&](int v) { return thr >= 0.0 && h.I2[v] == 1; }, D, P);
         else
             write_row(g, tab, r, s,
                       [&](int t) { return h.I2[t] == 1 ? d2b(D[t]) : INF_BITS; },
@@ -1520,7 +1538,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
         }
         __syncthreads();
         if (tslot >= 0)
-            tie_finalize(tie, tslot, n, lane, [&](int v) { return thr >= 0.0 && index2[v] != 0; }, P);
+            tie_finalize(tie, tslot, n, lane, [&](int v) { return thr >= 0.0 && index2[v] != 0; },
+                         [&](int v) { return thr >= 0.0 && index2[v] == 1; }, D, P);
         else
             write_row(g, tab, r, s,
                       [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },

@@ -40,7 +40,7 @@ EXPORTS = [
     "shd_rowstore_get", "shd_rowstore_store", "shd_rowstore_store_row", "shd_rowstore_increment",
     "shd_rowstore_size", "shd_rowstore_min_latency", "shd_rowstore_memory_bytes",
     "shd_pe_host_alloc", "shd_pe_host_free", "shd_pe_tune", "shd_pe_get_path",
-    "shd_rowstore_foreach", "shd_rowstore_store_rows",
+    "shd_rowstore_foreach", "shd_rowstore_store_rows", "shd_pe_put_rows", "shd_pe_row_checksums",
 ]
 
 
@@ -69,7 +69,7 @@ class Stats(C.Structure):
                 ("denseSweeps", C.c_int64), ("denseFlops", C.c_double),
                 ("batched", C.c_int32), ("batchLanes", C.c_int32), ("nShards", C.c_int32),
                 ("msGather", C.c_double), ("rowsTieEarly", C.c_int64), ("batchWaves", C.c_int32),
-                ("batchPostWaves", C.c_int32)]
+                ("batchPostWaves", C.c_int32), ("rowsTieRepaired", C.c_int64)]
 
 
 class EngineError(RuntimeError):
@@ -154,6 +154,8 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_get_path": (C.c_int, [vp, i32, i32, vp, i32, vp]),
         "shd_rowstore_foreach": (i64, [vp, vp, vp]),
         "shd_rowstore_store_rows": (C.c_int, [vp, vp, i32, vp, vp, vp, i64, i32, vp, i32, vp]),
+        "shd_pe_put_rows": (C.c_int, [vp, i32, i32, vp, vp, vp, vp, vp]),
+        "shd_pe_row_checksums": (C.c_int, [vp, i32, i32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -208,6 +210,37 @@ def kernel_source_hash() -> str:
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+_CK_K, _CK_C = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xD1B54A32D192ED03)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def row_checksums_host(rows: dict) -> np.ndarray:
+    """numpy twin of shd_pe_row_checksums (k_row_checksums, pe_aux.hip) over
+    rows as get_rows returns them (count x T per field): per row the wrapping
+    sum over entries j and fields f of splitmix64(bits ^ (j*K + f*C))."""
+    lat = np.atleast_2d(rows["lat"])
+    count, T = lat.shape
+    kj = np.arange(T, dtype=np.uint64) * _CK_K
+    fields = [(rows["lat"], 1), (rows["rel"], 2), (rows["hops"], 3), (rows["flags"], 4)]
+    if rows.get("pred") is not None:
+        fields.append((rows["pred"], 5))
+    out = np.zeros(count, np.uint64)
+    with np.errstate(over="ignore"):
+        for a, f in fields:
+            a = np.atleast_2d(a)
+            if a.dtype == np.float64:
+                bits = a.view(np.uint64)
+            else:       # i32 / u8 zero-extended, as the kernel does
+                bits = a.view(np.uint32 if a.dtype.itemsize == 4 else np.uint8).astype(np.uint64)
+            out += _mix64(bits ^ (kj + np.uint64(f) * _CK_C)[None, :]).sum(axis=1, dtype=np.uint64)
+    return out
 
 
 def strerror(code: int) -> str:
@@ -274,6 +307,29 @@ class Engine:
 
     def comm_init(self, uid: bytes):
         self._chk(self._lib.shd_pe_comm_init(self.h, uid, len(uid)), "shd_pe_comm_init")
+
+    def row_checksums(self, start: int, count: int) -> np.ndarray:
+        """shd_pe_row_checksums: 64-bit fingerprint of rows [start, start+count)
+        computed on the device (same formula as row_checksums_host)."""
+        out = np.empty(count, np.uint64)
+        self._chk(self._lib.shd_pe_row_checksums(self.h, int(start), int(count), _p(out)),
+                  "shd_pe_row_checksums")
+        return out
+
+    def put_rows(self, start: int, rows: dict):
+        """shd_pe_put_rows: another shard's rows [start, start+count) from host
+        buffers into this engine's full table (host-transport assembly)."""
+        lat = np.ascontiguousarray(rows["lat"], np.float64)
+        count = lat.shape[0]
+        rel = np.ascontiguousarray(rows["rel"], np.float64)
+        hops = np.ascontiguousarray(rows["hops"], np.int32)
+        flags = np.ascontiguousarray(rows["flags"], np.uint8)
+        pred = np.ascontiguousarray(rows["pred"], np.int32) if self.store_pred else None
+        for a in (rel, hops, flags) + ((pred,) if pred is not None else ()):
+            if a.shape != (count, self.T):
+                raise ValueError(f"put_rows: field of shape {a.shape}, want {(count, self.T)}")
+        self._chk(self._lib.shd_pe_put_rows(self.h, int(start), int(count), _p(lat), _p(rel), _p(hops),
+                                            _p(pred), _p(flags)), "shd_pe_put_rows")
 
     def close(self):
         if getattr(self, "h", None):

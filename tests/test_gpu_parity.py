@@ -50,6 +50,9 @@ def _check_engine(E, oracle_mod, top, att, sources=None, force=0, debug_flags=0)
         _assert_rows_equal(g, {k: v[i] for k, v in exp.items()}, f"row {s}")
     st = eng.stats()
     eng.close()
+    if not os.environ.get("SHDPE_TIE_CORRUPT"):
+        # the exact kernels' tie-slot cross-check never fires on a correct run
+        assert st["rowsTieRepaired"] == 0, st
     return st
 
 
@@ -672,38 +675,23 @@ def test_batched_kernel_each_lb(E, oracle_mod, monkeypatch, lb, wpe, case):
         assert st["rowsExact"] == 0
 
 
-@pytest.mark.xfail(strict=False, reason="opt-in experimental knobs (SHDPE_BATCH_COOP / SHDPE_BATCH_POST_SUB): "
-                   "one r04t run gave a wrong row at coop 2 + post over half batches that did not "
-                   "reproduce; not on any default path (profiles/r04_ab_notes.txt)")
-@pytest.mark.parametrize("coop,sub,lb", [(2, 0, 16), (4, 0, 16), (1, 1, 16), (2, 1, 16), (4, 2, 16),
-                                         (2, 0, 8), (4, 1, 8)])
-@pytest.mark.parametrize("wpe", [4, 8])
-@pytest.mark.parametrize("case", ["power_law", "quantized"])
-def test_batched_cooperative_relax(E, oracle_mod, monkeypatch, coop, sub, lb, wpe, case):
-    """Small shards: the relax kernel with coop workgroups per LB-16 / LB-8
-    batch (shared dist array and published near bitmaps in uncached memory,
-    a memory-side barrier per phase) and the post kernel over 2^sub lane
-    slices of each batch; bit-exact with the oracle, tie rows included."""
-    monkeypatch.setenv("SHDPE_BATCH_COOP", str(coop))
-    monkeypatch.setenv("SHDPE_BATCH_POST_SUB", str(sub))
-    monkeypatch.setenv("SHDPE_BATCH_LB", str(lb))
-    monkeypatch.setenv("SHDPE_BATCH_WPE", str(wpe))
-    if case == "power_law":
-        top = G.power_law(8000, m=3, seed=16)
-        att = G.sample_attached(top.n, 1203, seed=5)
-        srcs = att[::3]
+@pytest.mark.parametrize("case", ["batched", "sparse"])
+def test_tie_slot_cross_check_repairs(E, oracle_mod, monkeypatch, case):
+    """Early-stop tie rows: the exact kernel checks every vertex it popped
+    against the exported distance of the same row (a slot holding another
+    source's or a stale distance array -- the round-4 r04t symptom, latencies
+    below the true distance -- fails it).  SHDPE_TIE_CORRUPT halves one
+    slot's exported distances after the relevance scan: the row must be
+    caught (rowsTieRepaired), recomputed by the full emulation, and every row
+    stays bit-exact with the oracle."""
+    monkeypatch.setenv("SHDPE_TIE_CORRUPT", "1")
+    if case == "batched":
+        top, att, force = G.random_sparse(600, 6, seed=216, quantum=1.0), np.arange(599), 5
     else:
-        top, att, srcs = G.random_sparse(600, 6, seed=216, quantum=1.0), np.arange(599), None
-    st = _check_engine(E, oracle_mod, top, att, sources=srcs, force=5, debug_flags=E.DEBUG_ENV)
-    assert st["batched"] == 1 and st["batchLanes"] == lb and st["batchWaves"] == wpe
-    if case == "quantized":
-        assert st["rowsExact"] > 0
-    else:
-        # tie-free: a batch reaches the exact kernel only if its relaxation
-        # failed (a group barrier timed out, or near vertices were lost and
-        # the post kernel's Bellman check fired) -- the phase-alternating
-        # publication buffers keep that from happening
-        assert st["rowsExact"] == 0
+        top, att, force = G.rgg(2000, seed=9, quantum=0.05), None, 1
+        att = np.arange(top.n, dtype=np.int32)
+    st = _check_engine(E, oracle_mod, top, att, force=force, debug_flags=E.DEBUG_ENV)
+    assert st["rowsTieEarly"] > 0 and st["rowsTieRepaired"] >= 1, st
 
 
 def test_tune_with_fewer_scratch_slots_than_grid(E, oracle_mod, monkeypatch):

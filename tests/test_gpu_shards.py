@@ -116,19 +116,102 @@ def test_multiprocess_shard_engines(E):
         e.close()
 
 
-def test_c4_two_shards_full_size(E):
-    """C4 in two logical shards (LB and batch plan per shard) == one shard."""
+def _same_blocks(a_eng, b_eng, ctx, block=1024):
+    """Whole tables byte-identical, all five fields, in row blocks."""
+    T = a_eng.T
+    for p0 in range(0, T, block):
+        c = min(block, T - p0)
+        _same(a_eng.get_rows(p0, c), b_eng.get_rows(p0, c), f"{ctx} rows {p0}..{p0 + c}")
+
+
+@pytest.fixture(scope="module")
+def c4_one(E):
+    """The 1-shard C4 engine (headline config), computed once for the
+    full-size shard tests; its device fingerprints equal the numpy twin's."""
     top, att = G.make_config("c4")
     one = E.Engine(top, att)
+    one.tune()
     one.compute_all()
+    ck = one.row_checksums(0, one.T)
+    probe = one.get_rows(0, 64)
+    assert np.array_equal(ck[:64], E.row_checksums_host(probe))
+    yield top, att, one, ck
+    one.close()
+
+
+def test_c4_two_shards_full_size(E, c4_one):
+    """C4 in two logical shards (LB 16, batch plan per shard) == one shard,
+    whole table, all fields."""
+    top, att, one, ck = c4_one
     two = E.Engine(top, att, devices=[0, 0])
     two.compute_all()
-    rng = np.random.default_rng(5)
-    for p in np.sort(rng.choice(att.shape[0], 48, replace=False)):
-        a, b = one.get_rows(int(p), 1), two.get_rows(int(p), 1)
-        _same(a, b, f"c4 row {p}")
-    one.close()
+    _same_blocks(one, two, "c4 x2")
+    assert np.array_equal(two.row_checksums(0, two.T), ck)
     two.close()
+
+
+@pytest.mark.parametrize("wpe", ["tune", "4", "8"])
+def test_c4_eight_shards_full_size(E, c4_one, monkeypatch, wpe):
+    """C4 in eight logical shards = what each rank of the 8-GPU run computes
+    (2,048 rows, LB 8 batches, the tune's variant pick -- and each of the two
+    variants forced): whole table byte-identical to one engine's, before and
+    after the gather, and the device fingerprints agree."""
+    top, att, one, ck = c4_one
+    dbg = 0
+    if wpe != "tune":
+        monkeypatch.setenv("SHDPE_BATCH_WPE", wpe)
+        dbg = E.DEBUG_ENV
+    eng = E.Engine(top, att, devices=[0] * 8, debug_flags=dbg)
+    assert list(eng.shard_bounds()) == [2048 * g for g in range(9)]
+    if wpe == "tune":
+        eng.tune()
+    eng.reset_stats()
+    eng.compute_all()
+    st = eng.stats()
+    assert st["batched"] == 1 and st["batchLanes"] == 8 and st["rowsExact"] == 0, st
+    if wpe != "tune":
+        assert st["batchWaves"] == int(wpe)
+    _same_blocks(one, eng, f"c4 x8 wpe {wpe}")
+    eng.gather()
+    assert np.array_equal(eng.row_checksums(0, eng.T), ck)
+    eng.close()
+
+
+def test_put_rows_host_transport_and_checksums(E):
+    """Two shardIndex / shardCount engines (one per rank in bench.py's
+    one-GPU rehearsal): fingerprints of the owners' blocks == the 1-engine
+    table's; each engine lands the other's rows through shd_pe_put_rows
+    (host transport) and then reads the whole table byte-identical to one
+    engine, with matching device fingerprints.  Own rows are refused."""
+    top, att, force = _shard_case("batched")
+    one = E.Engine(top, att, force_mode=force)
+    one.compute_all()
+    ref = _all_rows(one)
+    ref_ck = one.row_checksums(0, one.T)
+    assert np.array_equal(ref_ck, E.row_checksums_host(ref))
+    one.close()
+    engs = [E.Engine(top, att, force_mode=force, shard_index=i, shard_count=2) for i in range(2)]
+    for e in engs:
+        e.compute_all()
+    own = np.concatenate([e.row_checksums(*e.owned) for e in engs])
+    assert np.array_equal(own, ref_ck)
+    for a, b in ((0, 1), (1, 0)):
+        s, c = engs[b].owned
+        half = c // 2                     # two puts: the table is assembled on the second
+        engs[a].put_rows(s, engs[b].get_rows(s, half))
+        with pytest.raises(E.EngineError) as ei:
+            engs[a].get_rows(s + half, c - half)
+        assert ei.value.code == E.ENOTOWNED
+        engs[a].put_rows(s + half, engs[b].get_rows(s + half, c - half))
+    for e in engs:
+        _same(_all_rows(e), ref, "put_rows assembled")
+        assert np.array_equal(e.row_checksums(0, e.T), ref_ck)
+    s, c = engs[0].owned
+    with pytest.raises(E.EngineError) as ei:
+        engs[0].put_rows(s, {k: v[s:s + 1] for k, v in ref.items()})
+    assert ei.value.code == E.EINVAL
+    for e in engs:
+        e.close()
 
 
 # ---------------------------------------------------------------------------

@@ -205,3 +205,117 @@ def test_shard_plan(lib):
                 units = np.diff((b + unit - 1) // unit)
                 assert units.max() - units.min() <= 1
     assert list(plan_shards(16_384, 8, 16)) == [2048 * g for g in range(9)]
+
+
+def _fake_table(T, seed=7):
+    rng = np.random.default_rng(seed)
+    return {"lat": rng.random((T, T)) * 100, "rel": rng.random((T, T)),
+            "hops": rng.integers(-1, 30, (T, T)).astype(np.int32),
+            "flags": rng.integers(0, 32, (T, T)).astype(np.uint8),
+            "pred": rng.integers(-1, 5000, (T, T)).astype(np.int32)}
+
+
+class _FakeEngine:
+    """numpy stand-in with the engine calls shdpe.gather uses (row_checksums,
+    get_rows, put_rows, pinned_rows): a rank's table starts with only its own
+    block filled; `corrupt` flips one bit of the first foreign row it lands."""
+
+    def __init__(self, T, start, count, corrupt=False):
+        from shdpe.engine import row_checksums_host
+        self._ck = row_checksums_host
+        self.T, self.store_pred, self.corrupt = T, True, corrupt
+        full = _fake_table(T)
+        self.tab = {k: np.zeros_like(v) for k, v in full.items()}
+        for k, v in full.items():
+            self.tab[k][start:start + count] = v[start:start + count]
+
+    def row_checksums(self, s, c):
+        return self._ck({k: v[s:s + c] for k, v in self.tab.items()})
+
+    def pinned_rows(self, c):
+        return {k: np.empty((c,) + v.shape[1:], v.dtype) for k, v in self.tab.items()}
+
+    def get_rows(self, s, c, out):
+        for k, v in self.tab.items():
+            out[k][:c] = v[s:s + c]
+
+    def put_rows(self, s, rows):
+        for k, v in rows.items():
+            self.tab[k][s:s + v.shape[0]] = v
+        if self.corrupt:
+            self.tab["lat"].view(np.uint64)[s, 3] ^= np.uint64(1)
+            self.corrupt = False
+
+
+def _gather_worker(rank, world, port, corrupt_rank, q):
+    import torch.distributed as dist
+    sys.path[:0] = [os.path.join(ROOT, "shadow-1_amd"), ROOT]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from shdpe.engine import plan_shards
+    from shdpe.gather import gather_and_verify
+    T = 600
+    b = plan_shards(T, world, unit=16)
+    start, count = int(b[rank]), int(b[rank + 1] - b[rank])
+    eng = _FakeEngine(T, start, count, corrupt=rank == corrupt_rank)
+    res = gather_and_verify(eng, dist, rank, world, T, start, count, "host", dist.barrier)
+    full = _fake_table(T)
+    res["identical"] = all(np.array_equal(eng.tab[k], full[k]) for k in full)
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_gather(world, corrupt_rank):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 1000) + 7 * world + (corrupt_rank + 1)
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, corrupt_rank, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_verify_host_transport_gloo(lib, world):
+    """shdpe.gather on CPU gloo ranks (the bench's N > 1 assembly minus the
+    GPU): owners' row fingerprints exchanged, rows moved by host transport,
+    every rank's assembled table fingerprinted and compared -- verified, and
+    the table equals the union of the owners' blocks."""
+    res = _run_gather(world, corrupt_rank=-1)
+    for r in range(world):
+        assert res[r]["verified"] and res[r]["identical"], res[r]
+        assert res[r]["mismatched_rows"] == 0
+
+
+def test_gather_verify_detects_corruption_gloo(lib):
+    """One flipped bit in one landed row on rank 1: rank 1 reports that row,
+    and the max-over-ranks count makes rank 0's verdict fail too."""
+    res = _run_gather(2, corrupt_rank=1)
+    assert res[1]["mismatched_rows"] == 1 and not res[1]["verified"]
+    assert res[0]["mismatched_rows"] == 0 and res[0]["mismatched_rows_max_over_ranks"] == 1
+    assert not res[0]["verified"]
+
+
+def test_row_checksums_host_properties(lib):
+    """The fingerprint (shd_pe_row_checksums' numpy twin) is a function of
+    every field and of each entry's position."""
+    from shdpe.engine import row_checksums_host
+    t = _fake_table(40)
+    base = row_checksums_host(t)
+    assert np.unique(base).size == 40
+    for k in t:
+        u = {kk: vv.copy() for kk, vv in t.items()}
+        u[k][5, 7] = u[k][5, 8] if u[k][5, 7] != u[k][5, 8] else u[k][5, 7] + 1
+        ck = row_checksums_host(u)
+        assert ck[5] != base[5] and np.array_equal(np.delete(ck, 5), np.delete(base, 5)), k
+    u = {kk: vv.copy() for kk, vv in t.items()}
+    u["lat"][9, [2, 3]] = u["lat"][9, [3, 2]]            # swapped entries
+    assert row_checksums_host(u)[9] != base[9]
+    nopred = {k: v for k, v in t.items() if k != "pred"}
+    assert not np.array_equal(row_checksums_host(nopred), base)

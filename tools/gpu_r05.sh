@@ -1,18 +1,19 @@
 #!/bin/bash
-# Round-4 GPU pass.  Stages (space-separated in $STAGES):
+# Round-5 GPU pass.  Stages (space-separated in $STAGES):
 #   tests     pytest -m gpu (PYTEST_K filters)
 #   rehearse  BENCH_REHEARSE_ONE_GPU=1 bench.py --gpus 2: the self-launched
-#             N-rank flow on one GPU; asserts "n_gpus": 2
+#             N-rank flow on one GPU; asserts "n_gpus": 2 and a verified
+#             table assembly (allgather.verified, host transport)
 #   shard     per-rank shard times (tools/shard_time.py) for $SHARD_WL at
 #             N = $SHARD_NS, once per SHDPE_* setting in $SHARD_ENVS (';' list)
 #   bench     quick bench.py lines for $WLS (no CPU leg / extras)
 #   default   the driver's command (python bench.py, all legs)
 #   trace     rocprofv3 --kernel-trace --stats of quick bench lines for $WLS
 #   pmc       FETCH_SIZE / WRITE_SIZE / TCC hit+miss passes -> traffic_<wl>.json
-# usage: STAGES="tests bench" tools/gpu_r04.sh TAG
+# usage: STAGES="tests bench" tools/gpu_r05.sh TAG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R
-TAG=${1:-r04}; OUT=gpurun_out/$TAG; mkdir -p $OUT
+TAG=${1:-r05}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 WLS=${WLS:-c4}
 QUICK='--no-cpu --tie-stress= --secondary= --host-fill 0 --d2h-rows 0 --no-stream'
@@ -24,7 +25,7 @@ for st in ${STAGES:-tests bench}; do
     rc=$?; tail -3 $OUT/tests.log; [ $rc = 0 ] || { grep -E "FAIL|Error|error|assert" $OUT/tests.log | head -30; exit $rc; } ;;
   rehearse)
     BENCH_REHEARSE_ONE_GPU=1 timeout -k 10 300 python3 -u bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --tie-stress "" --secondary "" --host-fill 0 --no-stream > $OUT/rehearse.json 2> $OUT/rehearse.err || { tail -20 $OUT/rehearse.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$OUT/rehearse.json')); assert d['n_gpus']==2, d; print('rehearse n_gpus', d['n_gpus'], round(d['value']), 'rows/s', round(d['ms_per_step'],2), 'ms/step')" || exit 1 ;;
+    python3 -c "import json; d=json.load(open('$OUT/rehearse.json')); a=d.get('allgather', {}); assert d['n_gpus']==2 and a.get('verified'), d; print('rehearse n_gpus', d['n_gpus'], round(d['value']), 'rows/s', round(d['ms_per_step'],2), 'ms/step; allgather', a.get('transport'), round(a['ms']), 'ms verified', a['verified'])" || exit 1 ;;
   shard)
     IFS=';' read -ra ES <<< "${SHARD_ENVS:-X=0}"
     for e in "${ES[@]}"; do
@@ -64,11 +65,11 @@ for st in ${STAGES:-tests bench}; do
     done ;;
   pmc)
     for wl in ${WLS//,/ }; do
-      for PASS in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" ${EXTRA_PASSES}; do
+      for PASS in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum TCC_ATOMIC_sum" ${EXTRA_PASSES}; do
         T2=$(echo $PASS | tr ' ' '_' | cut -c1-40)
         (cd /tmp && TMPDIR=/tmp timeout -s KILL 150 rocprofv3 --pmc $PASS --output-format csv -d $R/$OUT/pmc_${wl}_$T2 -o pmc -- python3 $R/bench.py --workload $wl --steps 1 --warmup 0 $QUICK > $R/$OUT/pmc_${wl}_$T2.log 2>&1) || { echo "pmc pass $wl $PASS failed"; tail -5 $OUT/pmc_${wl}_$T2.log; exit 1; }
       done
-      python3 tools/traffic_json.py $OUT $wl $TAG $OUT/traffic_$wl.json || exit 1
+      python3 tools/traffic_json.py $OUT $wl $TAG $OUT/traffic_$wl.json $OUT/${TAG}_${wl}_pmc || exit 1
     done ;;
   esac
 done

@@ -1,6 +1,6 @@
 """Turn one workload's rocprofv3 PMC passes into profiles/traffic_<wl>.json.
 
-usage: python tools/traffic_json.py <pmc outdir> <workload> <tag> [out.json]
+usage: python tools/traffic_json.py <pmc outdir> <workload> <tag> [out.json [part-csv prefix]]
 
 Reads the counter_collection CSVs under <outdir>/pmc_<wl>_* (one launch of
 the dominant kernel per pass, bench.py --steps 1 --warmup 0), applies the
@@ -40,6 +40,7 @@ def main():
             per[(f, k)].append((int(r.get("Dispatch_Id") or 0), name, r))
     tot = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(lambda: defaultdict(set))
+    parts = defaultdict(lambda: defaultdict(float))   # split batch path: relax / post separately
     for (f, k), rs in per.items():
         ids = sorted({d for d, _, _ in rs})
         last = ids[-1]
@@ -53,6 +54,8 @@ def main():
             if d in keep:
                 tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k][r["Counter_Name"]].add((f, d))
+                if k == "k_batch_rows" and (", 1>(" in nm or ", 2>(" in nm):
+                    parts["relax" if ", 1>(" in nm else "post"][r["Counter_Name"]] += float(r["Counter_Value"])
     if not tot:
         sys.exit(f"no counters for the path kernels under {outdir}/pmc_{wl}_*")
     k = max(tot, key=lambda x: tot[x].get("FETCH_SIZE", 0.0))
@@ -80,6 +83,21 @@ def main():
         "tag": tag,
         "src_hash": kernel_source_hash(),
     }
+    if k == "k_batch_rows" and parts:
+        # per kernel of the split path (where the excess goes)
+        out["parts"] = {}
+        for pn, pc in parts.items():
+            pf, pw = pc.get("FETCH_SIZE", 0.0) * 1024, pc.get("WRITE_SIZE", 0.0) * 1024
+            ph, pm = pc.get("TCC_HIT_sum", 0.0), pc.get("TCC_MISS_sum", 0.0)
+            out["parts"][pn] = {"bytes": 2 * pf + pw, "read_bytes": 2 * pf, "write_bytes": pw,
+                                "l2_hit_rate": ph / (ph + pm) if ph + pm else None,
+                                "counters": dict(pc)}
+        if len(sys.argv) > 5:        # per-part counter CSVs: <prefix>_{relax,post}.csv
+            for pn, pc in parts.items():
+                with open(f"{sys.argv[5]}_{pn}.csv", "w") as f:
+                    f.write("counter,value_per_step\n")
+                    for cn in sorted(pc):
+                        f.write(f"{cn},{pc[cn]:.0f}\n")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
