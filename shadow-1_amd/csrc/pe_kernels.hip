@@ -922,7 +922,8 @@ __global__ __launch_bounds__(SP_THREADS) void k_sparse_rows(
 //
 // Consistency check (round 5): every vertex the emulation popped has its
 // final igraph distance in Dem, which must equal the exported distance of the
-// same row bit for bit.  A slot holding another source's (or a stale)
+// same row (distances are positive, so equal values are equal bits; the
+// source may read -0.0).  A slot holding another source's (or a stale)
 // distance array fails it: thr := NaN, k_tie_write leaves the row alone and
 // the engine recomputes it with the full emulation (ShdPeStats.rowsTieRepaired,
 // zero in every correct run).
@@ -938,7 +939,7 @@ __device__ __forceinline__ void tie_finalize(const TieBuf& tie, int slot, int n,
         const int fp = tp[v];
         if (fp >= 0 && (fp & TIE_AMB))
             tp[v] = reached(v) ? P[v] : -1;   // unreached: off every target's path
-        if (popped(v) && d2b(Dem[v]) != d2b(td[v])) bad = true;
+        if (popped(v) && Dem[v] != td[v]) bad = true;   // (value compare: the SoA kernel pops the source as -0.0)
     }
     if (__ballot(bad) && lane == 0) tie.thr[slot] = __longlong_as_double(0x7ff8000000000000ll);
 }

@@ -647,7 +647,7 @@ def test_batched_kernel_each_variant(E, oracle_mod, monkeypatch, wpe, case):
         assert st["rowsExact"] > 0
 
 
-@pytest.mark.parametrize("lb", [4, 8, 16])
+@pytest.mark.parametrize("lb", [4, 8, 16, 32])
 @pytest.mark.parametrize("wpe", [4, 8])
 @pytest.mark.parametrize("case", ["power_law", "quantized"])
 def test_batched_kernel_each_lb(E, oracle_mod, monkeypatch, lb, wpe, case):

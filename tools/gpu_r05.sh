@@ -6,6 +6,7 @@
 #             table assembly (allgather.verified, host transport)
 #   shard     per-rank shard times (tools/shard_time.py) for $SHARD_WL at
 #             N = $SHARD_NS, once per SHDPE_* setting in $SHARD_ENVS (';' list)
+#   envs      quick bench lines for $WLS per SHDPE_* setting in $ENVS (';' list)
 #   bench     quick bench.py lines for $WLS (no CPU leg / extras)
 #   default   the driver's command (python bench.py, all legs)
 #   trace     rocprofv3 --kernel-trace --stats of quick bench lines for $WLS
@@ -47,6 +48,18 @@ for st in ${STAGES:-tests bench}; do
           L=shadow-1_amd/libshdpe.so; [ $lib != new ] && L=shadow-1_amd/libshdpe_$lib.so
           SHDPE_LIB=$R/$L timeout -k 10 300 python3 -u bench.py --workload $wl --steps 3 --warmup 1 $QUICK > $OUT/ab_${wl}_$lib.json 2> $OUT/ab_${wl}_$lib.err || { tail -20 $OUT/ab_${wl}_$lib.err; exit 1; }
           line $OUT/ab_${wl}_$lib.json "$wl $lib #$rep"
+        done
+      done
+    done ;;
+  envs)
+    # quick bench lines for $WLS once per SHDPE_* setting in $ENVS (';' list), REPS rounds
+    IFS=';' read -ra ES <<< "${ENVS:-X=0}"
+    for wl in ${WLS//,/ }; do
+      for rep in $(seq 1 ${REPS:-1}); do
+        for e in "${ES[@]}"; do
+          T2=$(echo "$e" | tr ' =/' '_-_' | cut -c1-60)
+          env $e timeout -k 10 300 python3 -u bench.py --workload $wl --steps ${STEPS:-3} --warmup 1 $QUICK > $OUT/env_${wl}_$T2.json 2> $OUT/env_${wl}_$T2.err || { tail -20 $OUT/env_${wl}_$T2.err; exit 1; }
+          line $OUT/env_${wl}_$T2.json "$wl [$e] #$rep"
         done
       done
     done ;;
