@@ -58,8 +58,8 @@ __global__ __launch_bounds__(256) void k_self_paths(DevGraph g0, const int32_t* 
         if (L < bl || (L == bl && pos < bp)) { bl = L; bp = pos; br = g.rel[a]; }
     }
     if (lane == 0 && self) {
-        const double L = g.selfLat[v];
-        if (L < bl || (L == bl && sp < bp)) { bl = L; bp = sp; br = g.selfRel[v]; }
+        const double L = g.selfMinLat[v];
+        if (L < bl || (L == bl && sp < bp)) { bl = L; bp = sp; br = g.selfMinRel[v]; }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

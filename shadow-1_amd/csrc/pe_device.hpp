@@ -50,6 +50,8 @@ struct DevGraph {
     const double* selfLat;     // [n]
     const double* selfRel;     // [n]
     const uint8_t* hasSelf;    // [n]
+    const double* selfMinLat;  // [n] the self path's loop (several loops: newest of min latency)
+    const double* selfMinRel;  // [n]
     const int32_t* attached;   // [T]
     const uint8_t* isAttached; // [n]
     const uint32_t* heavyBits; // [ceil(n/32)] vertices with degree >= heavyDeg

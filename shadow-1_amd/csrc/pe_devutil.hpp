@@ -44,6 +44,8 @@ __device__ __forceinline__ DevGraph global_view(const DevGraph& g0) {
     g.selfLat = as_global(g0.selfLat);
     g.selfRel = as_global(g0.selfRel);
     g.hasSelf = as_global(g0.hasSelf);
+    g.selfMinLat = as_global(g0.selfMinLat);
+    g.selfMinRel = as_global(g0.selfMinRel);
     g.attached = as_global(g0.attached);
     g.isAttached = as_global(g0.isAttached);
     g.heavyBits = as_global(g0.heavyBits);

@@ -481,7 +481,7 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
     std::vector<int32_t> newOf, rp, ip;
     hvec<int32_t> col, o2i, icol;
     hvec<double> lat, rel, ilat, irel;
-    std::vector<double> vrel, sl, sr;
+    std::vector<double> vrel, sl, sr, sml, smr;
     std::vector<uint8_t> hs;
     std::vector<int32_t> att;
     const bool perm = oldOf != nullptr;
@@ -520,10 +520,11 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
         } else {
             for (int64_t a = 0; a < m; ++a) o2i[arcNew[a]] = arcNew[g0.outToIn[a]];
         }
-        vrel.resize(n); sl.resize(n); sr.resize(n); hs.resize(n);
+        vrel.resize(n); sl.resize(n); sr.resize(n); hs.resize(n); sml.resize(n); smr.resize(n);
         for (int32_t k = 0; k < n; ++k) {
             vrel[k] = g0.vrel[od[k]]; sl[k] = g0.selfLat[od[k]];
             sr[k] = g0.selfRel[od[k]]; hs[k] = g0.hasSelf[od[k]];
+            sml[k] = g0.selfMinLat[od[k]]; smr[k] = g0.selfMinRel[od[k]];
         }
         att.resize(pe->attached.size());
         for (size_t i = 0; i < att.size(); ++i) att[i] = newOf[pe->attached[i]];
@@ -539,7 +540,7 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
     std::vector<uint8_t> isAtt(n, 0);
     for (int32_t v : ATT) isAtt[v] = 1;
     int32_t *rowPtr, *dcol, *outToIn, *datt;
-    double *dlat, *drel, *dvrel, *dsl, *dsr;
+    double *dlat, *drel, *dvrel, *dsl, *dsr, *dsml, *dsmr;
     uint8_t *dhs, *ia;
     if ((rc = dev_upload(sh, &rowPtr, RP)) || (rc = dev_upload(sh, &dcol, COL)) ||
         (rc = dev_upload(sh, &dlat, LAT)) || (rc = dev_upload(sh, &drel, REL)) ||
@@ -547,6 +548,8 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
         (rc = dev_upload(sh, &dvrel, perm ? vrel : g0.vrel)) ||
         (rc = dev_upload(sh, &dsl, perm ? sl : g0.selfLat)) ||
         (rc = dev_upload(sh, &dsr, perm ? sr : g0.selfRel)) ||
+        (rc = dev_upload(sh, &dsml, perm ? sml : g0.selfMinLat)) ||
+        (rc = dev_upload(sh, &dsmr, perm ? smr : g0.selfMinRel)) ||
         (rc = dev_upload(sh, &dhs, perm ? hs : g0.hasSelf)) || (rc = dev_upload(sh, &datt, ATT)) ||
         (rc = dev_upload(sh, &ia, isAtt)))
         return rc;
@@ -568,6 +571,7 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
     }
     d.rowPtr = rowPtr; d.col = dcol; d.lat = dlat; d.rel = drel; d.outToIn = outToIn;
     d.vrel = dvrel; d.selfLat = dsl; d.selfRel = dsr; d.hasSelf = dhs; d.attached = datt;
+    d.selfMinLat = dsml; d.selfMinRel = dsmr;
     d.isAttached = ia;
     {
         const int hd = sh->cfg.heavyDeg;

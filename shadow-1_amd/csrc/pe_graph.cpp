@@ -144,6 +144,8 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     g->vrel.assign(n, 1.0);
     g->selfLat.assign(n, 0.0);
     g->selfRel.assign(n, 0.0);
+    g->selfMinLat.assign(n, 0.0);
+    g->selfMinRel.assign(n, 0.0);
     g->hasSelf.assign(n, 0);
     // topology.c:956-970 vertex packetloss range; NaN = absent (:330-349)
     if (d->vertexPacketLoss) {
@@ -181,23 +183,25 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     int64_t bad = INT64_MAX;
     for (int64_t x : firstBad) bad = std::min(bad, x);
     // self-loops in edge order: the newest one of a vertex is its (v, v)
-    // edge; nSelf counts them for the completeness rule
+    // edge (the (s, s) path fold, direct paths, adjacency); nSelf counts them
+    // for the completeness rule.  A self-loop never changes a distance, so
+    // several loops need no merge rule: the self path
+    // (_topology_computeShortestPathToSelf, topology.c:1582-1598) walks them
+    // newest first and keeps the first strict minimum = the newest loop of
+    // minimum latency (<= in edge order below)
     std::vector<int32_t> nSelf(n, 0);
-    std::vector<double> selfMin(n, INFINITY);
     for (int c = 0; c < NC; ++c) {
         for (int64_t e : loops[c]) {
             if (e > bad) break;
             const int32_t a = d->edgeFrom[e];
+            const double L = d->edgeLatency[e], R = 1.0 - d->edgePacketLoss[e];   // :437
             g->hasSelf[a] = 1;
-            nSelf[a]++;
-            selfMin[a] = std::min(selfMin[a], d->edgeLatency[e]);
-            g->selfLat[a] = d->edgeLatency[e];
-            g->selfRel[a] = 1.0 - d->edgePacketLoss[e];                 // :437
+            if (nSelf[a]++ == 0 || L <= g->selfMinLat[a]) { g->selfMinLat[a] = L; g->selfMinRel[a] = R; }
+            g->selfLat[a] = L;
+            g->selfRel[a] = R;
         }
     }
     if (bad != INT64_MAX) return SHD_PE_EINVAL;
-    for (int32_t v = 0; v < n; ++v)
-        if (nSelf[v] > 1 && g->selfLat[v] != selfMin[v]) return SHD_PE_EMULTI;
     // row pointers; chunk c writes row v from offset rowPtr[v] + (arcs of v
     // in chunks < c): every row keeps edge-id order, as the serial fill
     g->rowPtr.assign(n + 1, 0);
@@ -341,7 +345,7 @@ int host_self_path(const HostGraph& g, int32_t v, double* lat, double* rel) {
     const int32_t b = g.rowPtr[v], e = g.rowPtr[v + 1];
     int32_t a = b;
     for (; a < e && g.col[a] < v; ++a) visit(g.lat[a], g.rel[a]);
-    if (g.hasSelf[v]) visit(g.selfLat[v], g.selfRel[v]);
+    if (g.hasSelf[v]) visit(g.selfMinLat[v], g.selfMinRel[v]);
     for (; a < e; ++a) visit(g.lat[a], g.rel[a]);
     if (!any && g.nEdges == 0) return SHD_PE_ENOEDGE;
     if (lat) *lat = 2.0 * minLatency;               // :1640

@@ -42,7 +42,9 @@ struct HostGraph {
     hvec<int32_t> outToIn;
     // vertex data
     std::vector<double> vrel;       // 1 - packetloss, 1.0 when absent/NaN
-    std::vector<double> selfLat, selfRel;
+    std::vector<double> selfLat, selfRel;        // newest self-loop: igraph_get_eid(v, v)
+    std::vector<double> selfMinLat, selfMinRel;  // several loops: the one the self path
+                                                 // takes (first strict minimum, newest first)
     std::vector<uint8_t> hasSelf;
     bool isComplete = false;
     // multigraphs only (empty otherwise): per vertex the incident EDGE count

@@ -241,6 +241,24 @@ def with_parallel_edges(top: Topology, frac: float, seed: int, consistent: bool 
                     name=top.name + ("_multi" if consistent else "_multi_bad"))
 
 
+def with_parallel_loops(top: Topology, frac: float, seed: int) -> Topology:
+    """Extra self-loops on a fraction of the looped vertices, one or two
+    each, appended (newest), with latencies below, equal to or above the
+    existing loop's: any order is legal (a loop never changes a distance; the
+    (s, s) fold takes the newest loop, the self path the newest of minimum
+    latency)."""
+    rng = np.random.default_rng(seed)
+    loops = np.flatnonzero(top.src == top.dst)
+    pick = rng.choice(loops, size=max(1, int(frac * loops.shape[0])), replace=False)
+    sel = np.concatenate([pick, pick[rng.random(pick.shape[0]) < 0.4]])
+    f = rng.choice([0.5, 1.0, 1.0, 2.0], size=sel.shape[0])
+    return Topology(n=top.n, directed=top.directed, src=np.concatenate([top.src, top.src[sel]]),
+                    dst=np.concatenate([top.dst, top.dst[sel]]),
+                    latency=np.concatenate([top.latency, top.latency[sel] * f]),
+                    loss=np.concatenate([top.loss, rng.uniform(0.0, 0.05, size=sel.shape[0])]),
+                    vloss=top.vloss, name=top.name + "_loops")
+
+
 def sample_attached(n: int, k: int, seed: int) -> np.ndarray:
     """Attached vertices (``verticesWithAttachedHosts``), sorted."""
     if k >= n:

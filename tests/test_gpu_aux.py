@@ -45,6 +45,8 @@ def _graphs():
     yield "power_law", G.power_law(5000, m=3, seed=7, quantum=0.5)
     yield "multigraph", G.with_parallel_edges(G.random_sparse(500, 6, seed=12, vloss=True, quantum=5.0), 0.3, seed=5)
     yield "multigraph_directed", G.with_parallel_edges(G.random_sparse(400, 6, seed=13, directed=True), 0.3, seed=6)
+    yield "parallel_loops", G.with_parallel_loops(G.random_sparse(400, 6, seed=14, quantum=5.0), 0.6, seed=8)
+    yield "parallel_loops_directed", G.with_parallel_loops(G.random_sparse(300, 6, seed=15, directed=True), 0.6, seed=9)
 
 
 @pytest.mark.parametrize("name,top", list(_graphs()), ids=[n for n, _ in _graphs()])

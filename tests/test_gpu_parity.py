@@ -242,6 +242,25 @@ def test_multigraph_rows(E, oracle_mod, directed, quantum, force):
         assert st["rowsExact"] > 0          # tie rows went through the igraph heap emulation
 
 
+@pytest.mark.parametrize("directed", [False, True], ids=["undirected", "directed"])
+@pytest.mark.parametrize("force", [0, 5], ids=["sparse", "batched"])
+def test_parallel_self_loops_rows(E, oracle_mod, directed, force):
+    """Several self-loops per vertex in any latency order (the newest may be
+    the slowest): accepted; every row bit-exact against the oracle -- the
+    (s, s) entry folds the newest loop (igraph_get_eid) -- and the direct
+    (s, s) lookup agrees."""
+    top = G.with_parallel_loops(G.random_sparse(300, 5, seed=51, directed=directed, vloss=True), 0.7, seed=3)
+    loops = top.src == top.dst
+    assert np.bincount(top.src[loops], minlength=top.n).max() >= 3
+    att = np.arange(0, 300, 2, dtype=np.int32)
+    _check_engine(E, oracle_mod, top, att, force=force)
+    eng = E.Engine(top, att)
+    og = oracle_mod.OracleGraph(top)
+    for v in range(0, 300, 7):
+        assert eng.direct_path(v, v) == og.direct(v, v), v
+    eng.close()
+
+
 def test_multigraph_complete_direct_rows(E, oracle_mod):
     """Complete multigraphs take the direct rows: every entry is the newest
     parallel edge's (latency, reliability), as _topology_lookupDirectPath
