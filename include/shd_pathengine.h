@@ -277,6 +277,18 @@ int shd_pe_put_rows(ShdPe* pe, int32_t start, int32_t count, const double* lat, 
  * assembled table after it.  No reference counterpart. */
 int shd_pe_row_checksums(ShdPe* pe, int32_t start, int32_t count, uint64_t* out);
 
+/* The whole-table path-cache fill in one pass: rows 0..T-1 (computed first
+ * if needed; a sharded engine must be gathered) into an EMPTY row store, with
+ * exactly the result of shd_rowstore_store_rows over every row in position
+ * order (isComplete from the graph, no prefersDirectPaths adjacency --
+ * topology.c:1805-1864 per row).  The device packs the store's triangular
+ * row image (shd_rowstore_image_layout: 17 B per unordered pair instead of
+ * 34 B of two rows) and one DMA lands it in page-locked memory the store
+ * adopts.  rowResult (optional, T entries): each row's store_row result.
+ * msOut (optional, 3 entries): ms of allocation, device pack, DMA. */
+struct ShdRowStore;
+int shd_pe_fill_rowstore(ShdPe* pe, struct ShdRowStore* st, int32_t* rowResult, double* msOut);
+
 /* Wait for outstanding device work of this engine. */
 int shd_pe_synchronize(ShdPe* pe);
 
@@ -370,6 +382,22 @@ int shd_rowstore_store_rows(ShdRowStore* st, const int32_t* srcs, int32_t count,
                             const double* lat, const double* rel, const uint8_t* flags,
                             int64_t ld, int32_t isComplete, const uint8_t* adjacent,
                             int32_t nThreads, int32_t* rowResult);
+/* Bulk fill from a row IMAGE (the engine builds it on the device,
+ * shd_pe_fill_rowstore): the store's own row layout, every triangular row a
+ * (attached ordinal, len T - a) at offsets[a] from shd_rowstore_image_layout
+ * (T + 1 entries, 64-B aligned): SHD_ROWSTORE_IMAGE_HEADER bytes the store
+ * fills, lat f64[len], rel f64[len], state u8[len] (SHD_ROWSTORE_S_* bits).
+ * Slot k of row a is the unordered pair (a, a + k).  adopt_image hands an
+ * image to an EMPTY store (SHD_PE_EINVAL otherwise) with its entry count and
+ * minimum stored latency; release(ctx, image) frees it with the store. */
+#define SHD_ROWSTORE_IMAGE_HEADER 64
+#define SHD_ROWSTORE_S_STORED   0x1u
+#define SHD_ROWSTORE_S_DIRECT   0x2u
+#define SHD_ROWSTORE_S_REVERSED 0x4u   /* stored under (larger, smaller) ordinal */
+int shd_rowstore_image_layout(int32_t T, int64_t* offsets);
+int shd_rowstore_adopt_image(ShdRowStore* st, void* image, int64_t bytes,
+                             void (*release)(void* ctx, void* image), void* ctx, int64_t stored,
+                             double minLatency);
 /* topology_incrementPathPacketCounter on a cached entry: 0, or -1 if absent. */
 int shd_rowstore_increment(ShdRowStore* st, int32_t s, int32_t d);
 int64_t shd_rowstore_size(const ShdRowStore* st);

@@ -13,6 +13,7 @@
 
 #include "pe_device.hpp"
 #include "pe_devutil.hpp"
+#include "shd_pathengine.h"
 
 namespace shdpe {
 
@@ -253,6 +254,103 @@ void launch_row_checksums(const DevTable& tab, int64_t firstLocal, int32_t rows,
     if (rows <= 0) return;
     hipLaunchKernelGGL(k_row_checksums, dim3(rows), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        tab, firstLocal, dOut);
+}
+
+}  // namespace shdpe
+
+namespace shdpe {
+
+// ---------------------------------------------------------------------------
+// Path-cache image (shd_pe_fill_rowstore): the triangular row store of
+// pe_rowstore.cpp filled from the whole table exactly as
+// shd_rowstore_store_rows over rows 0, 1, ..., T-1 in order would fill it
+// (topology.c:1805-1864 per row, :1307-1386 per target, no complete graph,
+// no prefersDirectPaths): slot (a, a + k) takes row a's entry a + k when that
+// fold succeeded (neither F_UNREACHABLE nor F_NOEDGE), else row a + k's
+// entry a (stored under the reversed key), else stays empty.  One workgroup
+// per triangular row: coalesced along row a, the reverse column gathered
+// only for the (rare) failed forward entries.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack_rowstore(DevTable tab0, const int64_t* __restrict__ off,
+                                                       uint8_t* __restrict__ img,
+                                                       unsigned long long* __restrict__ acc) {
+    const DevTable tab = global_view(tab0);
+    __shared__ unsigned long long cnt[4], mnb[4];
+    const int64_t T = tab.T;
+    const int64_t a = blockIdx.x, len = T - a;
+    uint8_t* base = img + off[a] + SHD_ROWSTORE_IMAGE_HEADER;
+    double* L = reinterpret_cast<double*>(base);
+    double* R = L + len;
+    uint8_t* S = reinterpret_cast<uint8_t*>(R + len);
+    constexpr uint8_t FAILED = F_UNREACHABLE | F_NOEDGE;
+    unsigned long long c = 0, mn = INF_BITS;
+    for (int64_t k = threadIdx.x; k < len; k += 256) {
+        const int64_t b = a + k;
+        const size_t fo = (size_t)a * T + b;
+        double lat = 0.0, rel = 0.0;
+        uint8_t s = 0;
+        if (!(tab.flags[fo] & FAILED)) {
+            lat = tab.lat[fo];
+            rel = tab.rel[fo];
+            s = SHD_ROWSTORE_S_STORED;
+        } else if (k > 0) {
+            const size_t ro = (size_t)b * T + a;
+            if (!(tab.flags[ro] & FAILED)) {
+                lat = tab.lat[ro];
+                rel = tab.rel[ro];
+                s = SHD_ROWSTORE_S_STORED | SHD_ROWSTORE_S_REVERSED;
+            }
+        }
+        L[k] = lat;
+        R[k] = rel;
+        S[k] = s;
+        if (s) {
+            ++c;
+            const unsigned long long lb = (unsigned long long)__double_as_longlong(lat);
+            mn = lb < mn ? lb : mn;      // stored latencies are > 0: bit order = value order
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        c += __shfl_xor(c, d, 64);
+        const unsigned long long o = __shfl_xor(mn, d, 64);
+        mn = o < mn ? o : mn;
+    }
+    if ((threadIdx.x & 63) == 0) { cnt[threadIdx.x >> 6] = c; mnb[threadIdx.x >> 6] = mn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long cc = 0, m = INF_BITS;
+        for (int w = 0; w < 4; ++w) { cc += cnt[w]; m = mnb[w] < m ? mnb[w] : m; }
+        if (cc) atomicAdd(&acc[0], cc);
+        if (m != INF_BITS) atomicMin(&acc[1], m);
+    }
+}
+
+// per source row: 1 when no target's fold failed (F_NOEDGE; unreachable
+// targets do not count), topology.c:1815-1859's isAllSuccess
+__global__ __launch_bounds__(256) void k_rows_all_success(DevTable tab0, int32_t* __restrict__ out) {
+    const DevTable tab = global_view(tab0);
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * (size_t)tab.T;
+    int b = 0;
+    for (int64_t j = threadIdx.x; j < tab.T; j += 256) b |= (tab.flags[base + j] & F_NOEDGE) != 0;
+    if (b) bad = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = bad ? 0 : 1;
+}
+
+void launch_pack_rowstore(const DevTable& tab, const int64_t* dOff, uint8_t* dImg,
+                          unsigned long long* dAcc, void* stream) {
+    if (tab.T <= 0) return;
+    hipLaunchKernelGGL(k_pack_rowstore, dim3((unsigned)tab.T), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), tab, dOff, dImg, dAcc);
+}
+
+void launch_rows_all_success(const DevTable& tab, int32_t* dOut, void* stream) {
+    if (tab.T <= 0) return;
+    hipLaunchKernelGGL(k_rows_all_success, dim3((unsigned)tab.T), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), tab, dOut);
 }
 
 }  // namespace shdpe

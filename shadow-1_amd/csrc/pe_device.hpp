@@ -227,6 +227,13 @@ void launch_self_paths(const DevGraph& g, const int32_t* dVerts, int32_t count, 
 void launch_pairs(const DevGraph& g, const int32_t* dSrc, const int32_t* dDst, int64_t count,
                   int mode, double* dLat, double* dRel, uint8_t* dFlags, void* stream);
 void launch_incident_min(const DevGraph& g, const int32_t* dEdgeCount, int32_t* dOut, void* stream);
+// path-cache image of the whole table (rows 0..T-1 of `tab`, rowStart 0) in
+// the row store's layout (dOff: shd_rowstore_image_layout); dAcc[0] += stored
+// entries, dAcc[1] = min stored latency bits (init INF_BITS)
+void launch_pack_rowstore(const DevTable& tab, const int64_t* dOff, uint8_t* dImg,
+                          unsigned long long* dAcc, void* stream);
+// per table row: 1 = no F_NOEDGE target (isAllSuccess of topology.c:1815-1859)
+void launch_rows_all_success(const DevTable& tab, int32_t* dOut, void* stream);
 // 64-bit fingerprint per table row (local rows firstLocal .. + rows), pe_aux.hip
 void launch_row_checksums(const DevTable& tab, int64_t firstLocal, int32_t rows, uint64_t* dOut,
                           void* stream);

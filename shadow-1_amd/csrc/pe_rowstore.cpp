@@ -40,7 +40,8 @@
 
 namespace {
 
-constexpr uint8_t S_STORED = 1, S_DIRECT = 2, S_REVERSED = 4;
+constexpr uint8_t S_STORED = SHD_ROWSTORE_S_STORED, S_DIRECT = SHD_ROWSTORE_S_DIRECT,
+                  S_REVERSED = SHD_ROWSTORE_S_REVERSED;
 
 // One triangular row: lat | rel | state, carved from an arena; the packet
 // counters (u64 per slot) are allocated on the row's first increment -- the
@@ -113,11 +114,14 @@ struct ShdRowStore {
     std::atomic<int64_t> bytes{0};
     std::mutex writer;
     Arena arena;                                         // rows (freed with the store)
+    // adopted row images (shd_rowstore_adopt_image), released with the store
+    std::vector<std::pair<void*, std::pair<void (*)(void*, void*), void*>>> images;
     ~ShdRowStore() {
         if (rows)
             for (int32_t a = 0; a < T; ++a)
                 if (TriRow* r = rows[a].load(std::memory_order_relaxed))
                     std::free(r->packets.load(std::memory_order_relaxed));
+        for (auto& im : images) im.second.first(im.second.second, im.first);
     }
 };
 
@@ -426,6 +430,53 @@ extern "C" int shd_rowstore_store_rows(ShdRowStore* st, const int32_t* srcs, int
     st->size.fetch_add(added, std::memory_order_relaxed);
     if (added) track_min(st, mn);          // every stored latency is > 0 here
     return err ? err : SHD_PE_OK;
+}
+
+// Row image (SHD_ROWSTORE_IMAGE_*): every triangular row a (len T - a) at
+// offsets[a], 64-B aligned: a 64-B header the store fills (the TriRow),
+// lat f64[len], rel f64[len], state u8[len] -- the layout make_row carves
+// from an arena, so an adopted image IS the store's rows.
+extern "C" int shd_rowstore_image_layout(int32_t T, int64_t* offsets) {
+    static_assert(sizeof(TriRow) <= SHD_ROWSTORE_IMAGE_HEADER, "");
+    if (T < 0 || !offsets) return SHD_PE_EINVAL;
+    int64_t o = 0;
+    for (int32_t a = 0; a < T; ++a) {
+        offsets[a] = o;
+        o += (SHD_ROWSTORE_IMAGE_HEADER + 17 * (int64_t)(T - a) + 63) & ~(int64_t)63;
+    }
+    offsets[T] = o;
+    return SHD_PE_OK;
+}
+
+extern "C" int shd_rowstore_adopt_image(ShdRowStore* st, void* image, int64_t bytes,
+                                        void (*release)(void* ctx, void* image), void* ctx,
+                                        int64_t stored, double minLatency) {
+    if (!st || !image || !release || stored < 0) return SHD_PE_EINVAL;
+    std::lock_guard<std::mutex> lk(st->writer);
+    if (st->size.load(std::memory_order_relaxed) != 0) return SHD_PE_EINVAL;
+    for (int32_t a = 0; a < st->T; ++a)
+        if (st->rows[a].load(std::memory_order_relaxed)) return SHD_PE_EINVAL;
+    std::vector<int64_t> off((size_t)st->T + 1);
+    shd_rowstore_image_layout(st->T, off.data());
+    if (bytes < off[st->T]) return SHD_PE_EINVAL;
+    char* base = static_cast<char*>(image);
+    for (int32_t a = 0; a < st->T; ++a) {
+        char* p = base + off[a];
+        const size_t len = (size_t)(st->T - a);
+        TriRow* r = new (p) TriRow();
+        p += SHD_ROWSTORE_IMAGE_HEADER;
+        r->lat = reinterpret_cast<double*>(p);
+        r->rel = reinterpret_cast<double*>(p + len * 8);
+        r->state = reinterpret_cast<std::atomic<uint8_t>*>(p + len * 16);
+        r->packets.store(nullptr, std::memory_order_relaxed);
+        r->len = len;
+        st->rows[a].store(r, std::memory_order_release);
+    }
+    st->images.push_back({image, {release, ctx}});
+    st->bytes.fetch_add(off[st->T], std::memory_order_relaxed);
+    st->size.store(stored, std::memory_order_relaxed);
+    if (stored) track_min(st, minLatency);
+    return SHD_PE_OK;
 }
 
 extern "C" int64_t shd_rowstore_size(const ShdRowStore* st) {

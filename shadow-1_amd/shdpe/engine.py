@@ -41,6 +41,7 @@ EXPORTS = [
     "shd_rowstore_size", "shd_rowstore_min_latency", "shd_rowstore_memory_bytes",
     "shd_pe_host_alloc", "shd_pe_host_free", "shd_pe_tune", "shd_pe_get_path",
     "shd_rowstore_foreach", "shd_rowstore_store_rows", "shd_pe_put_rows", "shd_pe_row_checksums",
+    "shd_rowstore_image_layout", "shd_rowstore_adopt_image", "shd_pe_fill_rowstore",
 ]
 
 
@@ -156,6 +157,9 @@ def load_library(path: str = LIB_PATH):
         "shd_rowstore_store_rows": (C.c_int, [vp, vp, i32, vp, vp, vp, i64, i32, vp, i32, vp]),
         "shd_pe_put_rows": (C.c_int, [vp, i32, i32, vp, vp, vp, vp, vp]),
         "shd_pe_row_checksums": (C.c_int, [vp, i32, i32, vp]),
+        "shd_rowstore_image_layout": (C.c_int, [i32, vp]),
+        "shd_rowstore_adopt_image": (C.c_int, [vp, vp, i64, vp, vp, i64, f64]),
+        "shd_pe_fill_rowstore": (C.c_int, [vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -488,6 +492,15 @@ class Engine:
         self._chk(self._lib.shd_pe_adjacent_pairs(self.h, _p(s), _p(d), s.shape[0], _p(out)),
                   "shd_pe_adjacent_pairs")
         return out
+
+    def fill_rowstore(self, store) -> tuple:
+        """shd_pe_fill_rowstore: the whole table into an empty RowStore in one
+        device pack + DMA; returns (per-row store_row results, ms of
+        allocation / pack / DMA)."""
+        res = np.empty(self.T, np.int32)
+        ms = np.zeros(3)
+        self._chk(self._lib.shd_pe_fill_rowstore(self.h, store.h, _p(res), _p(ms)), "shd_pe_fill_rowstore")
+        return res, {"alloc": ms[0], "pack": ms[1], "dma": ms[2]}
 
     def is_complete_device(self) -> bool:
         x = C.c_int32(0)

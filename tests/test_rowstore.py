@@ -230,3 +230,89 @@ def test_store_rows_rejects_bad_buffers():
         st.store_rows(att[:3], lat.astype(np.float32), rel, fl)
     with pytest.raises(Exception):
         st.store_rows(np.array([1, 2, 3], np.int32), lat, rel, fl)    # 1 is not attached
+
+
+def pack_image_model(lat, rel, flags):
+    """The row image shd_pe_fill_rowstore's k_pack_rowstore builds (pe_aux.hip),
+    restated in numpy from the whole T x T table: slot (a, a+k) = row a's
+    entry a+k if that fold succeeded, else row a+k's entry a stored under the
+    reversed key, else empty -- shd_rowstore_store_rows over rows 0..T-1."""
+    import ctypes as C
+    from shdpe.engine import load_library
+    T = lat.shape[0]
+    off = np.empty(T + 1, np.int64)
+    assert load_library().shd_rowstore_image_layout(T, off.ctypes.data_as(C.c_void_p)) == 0
+    img = np.zeros(int(off[T]), np.uint8)
+    ok = (flags & (F_UNREACHABLE | F_NOEDGE)) == 0
+    stored, mn = 0, np.inf
+    for a in range(T):
+        n = T - a
+        b = np.arange(a, T)
+        fwd = ok[a, b]
+        rev = ~fwd & (b > a) & ok[b, a]
+        L = np.where(fwd, lat[a, b], np.where(rev, lat[b, a], 0.0))
+        R = np.where(fwd, rel[a, b], np.where(rev, rel[b, a], 0.0))
+        S = np.where(fwd, 1, np.where(rev, 1 | 4, 0)).astype(np.uint8)
+        o = int(off[a]) + 64
+        img[o:o + 8 * n] = L.view(np.uint8)
+        img[o + 8 * n:o + 16 * n] = R.view(np.uint8)
+        img[o + 16 * n:o + 17 * n] = S
+        stored += int((S != 0).sum())
+        if (S != 0).any():
+            mn = min(mn, float(L[S != 0].min()))
+    return img, stored, (0.0 if stored == 0 else mn)
+
+
+def _random_table(T, seed, directed):
+    rng = np.random.default_rng(seed)
+    lat = rng.uniform(0.5, 50.0, (T, T))
+    rel = rng.uniform(0.9, 1.0, (T, T))
+    flags = np.zeros((T, T), np.uint8)
+    flags[rng.random((T, T)) < 0.08] = F_UNREACHABLE
+    if not directed:
+        flags = np.maximum(flags, flags.T)
+    d = rng.random(T) < 0.3
+    flags[d, d] = F_NOEDGE                              # missing (s, s) self-loops
+    return lat, rel, flags
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_adopted_image_equals_store_rows(directed):
+    """An image in the store's row layout (shd_rowstore_image_layout), built by
+    the pack rule shd_pe_fill_rowstore's kernel implements, adopted by an
+    empty store (shd_rowstore_adopt_image) answers every lookup, the size,
+    the minimum latency and the entry walk exactly as shd_rowstore_store_rows
+    over all rows in position order -- the layout and rule the GPU fill
+    relies on, pinned on the CPU."""
+    import ctypes as C
+    T, n = 70, 90
+    att = _attached(n, T, seed=3)
+    lat, rel, flags = _random_table(T, 11 + int(directed), directed)
+    ref = RowStore(n, att)
+    ref.store_rows(att, lat, rel, flags)
+    img, stored, mn = pack_image_model(lat, rel, flags)
+    st = RowStore(n, att)
+    lib = st._lib if hasattr(st, "_lib") else None
+    from shdpe.engine import load_library
+    lib = load_library()
+    REL = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p)
+    keep = REL(lambda ctx, p: None)                     # the test owns the buffer
+    rc = lib.shd_rowstore_adopt_image(st.h, img.ctypes.data_as(C.c_void_p), img.nbytes,
+                                      C.cast(keep, C.c_void_p), None, stored, mn)
+    assert rc == 0
+    assert st.size() == ref.size() == stored
+    assert st.min_latency() == ref.min_latency()
+    assert sorted(st.items()) == sorted(ref.items())
+    for s in att[::7]:
+        for d in att[::5]:
+            assert st.get(int(s), int(d)) == ref.get(int(s), int(d)), (s, d)
+    # a second image, or one into a store with entries, is refused
+    assert lib.shd_rowstore_adopt_image(st.h, img.ctypes.data_as(C.c_void_p), img.nbytes,
+                                        C.cast(keep, C.c_void_p), None, stored, mn) != 0
+    assert lib.shd_rowstore_adopt_image(ref.h, img.ctypes.data_as(C.c_void_p), img.nbytes,
+                                        C.cast(keep, C.c_void_p), None, stored, mn) != 0
+    # the adopted rows take packet counters like any other
+    s, d = next((int(a), int(b)) for a in att for b in att if st.get(int(a), int(b)) is not None)
+    assert st.increment(s, d) == 0 and st.get(s, d)[3] == 1
+    st.close()
+    ref.close()
