@@ -86,6 +86,7 @@ struct Tuning {
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
     int debug = 0, streamWgPerCU = 16;
+    int tuneLog = 0;           // print shd_pe_tune's per-variant times (no kernel counters)
     int tieCorrupt = 0;        // tests only: scale one early-stop slot's exported distances
                                // after the relevance scan (exercises the tie-slot repair)
 };

@@ -180,6 +180,7 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_DEBUG", t.debug);
     gi("SHDPE_STREAM_WG_PER_CU", t.streamWgPerCU);
     gi("SHDPE_TIE_CORRUPT", t.tieCorrupt);
+    gi("SHDPE_TUNE_LOG", t.tuneLog);
 }
 
 extern "C" void shd_pe_default_options(ShdPeOptions* opt) {
@@ -1406,7 +1407,7 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
         sh->stats = keep;
         sh->stats.batchWaves = sh->bcfg.wpe;
         sh->stats.batchPostWaves = sh->bcfg.split ? cand[pk].wpe : 0;
-        if (pe->tu.debug)
+        if (pe->tu.debug || pe->tu.tuneLog)
             for (int k = 0; k < nc; ++k)
                 std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms (relax %.2f post %.2f)%s\n",
                              sh->gindex, w[k], ms[k], part[k][0], part[k][1],
@@ -1761,6 +1762,7 @@ static void host_free_cb(void*, void* p) { (void)hipHostFree(p); }
 
 extern "C" int shd_pe_fill_rowstore(ShdPe* pe, ShdRowStore* st, int32_t* rowResult, double* msOut) {
     if (!pe || !st) return SHD_PE_EINVAL;
+    if (shd_rowstore_size(st) != 0) return SHD_PE_EINVAL;   // (adopt_image re-checks under its lock)
     const int32_t T = (int32_t)pe->attached.size();
     int rc = ensure_rows(pe, 0, T);
     if (rc) return rc;
