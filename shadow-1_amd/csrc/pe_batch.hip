@@ -614,7 +614,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                     const int srcL = gbase + min(t + k, LB - 1);   // inside the group
                                     const int c = __shfl(mc[v], srcL, 64);
                                     ws[v][k] = __shfl(ml[v], srcL, 64);
-                                    xs[v][k] = c0 + t + k < deg[v] ? c : -1;
+                                    xs[v][k] = t + k < cn && c0 + t + k < deg[v] ? c : -1;   // (the chunk's own records)
                                 }
 #pragma unroll
                             for (int v = 0; v < BV; ++v)
@@ -930,7 +930,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                     const int srcL = gbase + min(t + k, LB - 1);
                                     const int c = __shfl(mc[v], srcL, 64);
                                     lw[v][k] = __shfl(ml[v], srcL, 64);
-                                    cu[v][k] = c0 + t + k < deg[v] ? c : -1;
+                                    cu[v][k] = t + k < cn && c0 + t + k < deg[v] ? c : -1;   // (a repeat would count as a tie)
                                 }
 #pragma unroll
                             for (int v = 0; v < BV; ++v)
