@@ -48,22 +48,9 @@ constexpr int BKP = 3;       // in-arcs per vertex per load batch (predecessor p
 // WPE = waves per SIMD the kernel is compiled for: 4 (128 VGPRs, one
 // 1024-thread workgroup per CU, two vertices interleaved per group) or 8
 // (64 VGPRs, two workgroups per CU, one vertex per group)
-// Experiment knobs (A/B builds through tools/build_variant.sh -D...): the
-// 4-wave variant on the pipelined loops, and its gather widths.
-#ifndef SHDPE_W4_PIPE
-#define SHDPE_W4_PIPE 0
-#endif
-#ifndef SHDPE_W4_BK
-#define SHDPE_W4_BK 3
-#endif
 template <int WPE> struct BCfg {
-    // software-pipelined loops (the 8- and 6-wave variants: one vertex per
-    // group); the 4-wave variant interleaves two vertices per group
-    static constexpr bool PIPE = WPE >= 6 || SHDPE_W4_PIPE;
     static constexpr int BV = WPE >= 6 ? 1 : 2;      // vertices interleaved per group
     static constexpr int SMAX = WPE >= 6 ? 8 : 16;   // label-walk stack: (entry, arc) pairs per thread
-    static constexpr int BKR = WPE >= 6 ? BK : SHDPE_W4_BK;    // pipelined loops' gather widths
-    static constexpr int BKQ = WPE >= 6 ? BKP : SHDPE_W4_BK;
 };
 constexpr int WALK_BUDGET = 2048;   // walk steps per target before the deep-tree sweeps
 // Lane policy of the relaxation: a vertex with ANY dirty lane below the
@@ -237,13 +224,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     constexpr int PT = PART;
     constexpr int BV = BCfg<WPE>::BV;
     constexpr int SMAX = BCfg<WPE>::SMAX;
-    // software pipelining of the light-vertex relax loop and the predecessor
-    // pass (next take's loads in flight): in the 8- and 6-wave variants
-    // (one vertex per group); the 4-wave variant (two per group) issues them
-    // at the next take's start (C4 N=8 per-rank shards: 24.5-24.8 ms with
-    // the tune's pipelined pick vs 23.0-23.2 without, r04ze)
-    constexpr bool PIPE = BCfg<WPE>::PIPE;
-    constexpr int BKR = BCfg<WPE>::BKR, BKQ = BCfg<WPE>::BKQ;
+    // the light-vertex relax loop and the predecessor pass are software-
+    // pipelined three takes deep with lane-distributed arc records (round 5:
+    // C4 N=1 106 -> 98.4 ms, N=8 shards 19.4 -> 18.9 ms same box, r05f;
+    // profiles/r05_ab_notes.txt); BKR / BKQ = dist gathers per vertex in flight
+    constexpr int BKR = BK, BKQ = BKP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int tieSlot[LB];
     __shared__ int laneRow[LB];           // table row of each lane (-1: pad)
@@ -506,247 +491,124 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 if (l == 0) i = atomicAdd(&ctl->qhead, BV);
                 return __shfl(i, gbase, 64);
             };
-            if constexpr (PIPE) {
-                // A three-stage software pipeline over the group's takes (BV
-                // vertices each).  The group's lanes hold ONE arc record per
-                // vertex (lane l: arc a0 + l of the vertex's first LB arcs --
-                // one coalesced LB x 16-B read per group instead of BK
-                // broadcast records per round and a dependent record round
-                // trip before every dist gather); the relaxing lanes take the
-                // heads by cross-lane reads.  Per take the group issues the
-                // records of the next take, the dist lines + row ranges of the
-                // one after, and the queue entries of the third, then relaxes
-                // the current vertices: their chain is the BKR-wide dist
-                // gathers only.  An entry past the queue end is u = -1 (takes
-                // rise monotonically, so a take whose first entry is -1 ends).
-                auto q_at = [&](int i) { return i < qn ? ld_wg(&Q[min(i, qc)]) : -1; };
-                auto ld_head = [&](int uu, unsigned long long& d, int& r0, int& r1) {
-                    const int uc = uu >= 0 ? uu : 0;
-                    const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
-                    const int x0 = g.rowPtr[uc], x1 = g.rowPtr[uc + 1];
-                    d = uu >= 0 ? d0 : INF_ENC;
-                    r0 = uu >= 0 ? x0 : 0;
-                    r1 = uu >= 0 ? x1 : 0;
-                };
-                auto ld_arc = [&](int a, int aEnd, int& c, double& w) {
-                    const bool ok = a < aEnd;
-                    const Arc A = g.arcs[ok ? a : 0];
-                    c = ok ? A.col : -1;
-                    w = A.lat;
-                };
-                int uC[BV], u1[BV], u2[BV], a0C[BV], a1C[BV], a01[BV], a11[BV], mcC[BV];
-                unsigned long long dbC[BV], db1[BV];
-                double mlC[BV];
+            // A three-stage software pipeline over the group's takes (BV
+            // vertices each).  The group's lanes hold ONE arc record per
+            // vertex (lane l: arc a0 + l of the vertex's first LB arcs --
+            // one coalesced LB x 16-B read per group instead of BK
+            // broadcast records per round and a dependent record round
+            // trip before every dist gather); the relaxing lanes take the
+            // heads by cross-lane reads.  Per take the group issues the
+            // records of the next take, the dist lines + row ranges of the
+            // one after, and the queue entries of the third, then relaxes
+            // the current vertices: their chain is the BKR-wide dist
+            // gathers only.  An entry past the queue end is u = -1 (takes
+            // rise monotonically, so a take whose first entry is -1 ends).
+            auto q_at = [&](int i) { return i < qn ? ld_wg(&Q[min(i, qc)]) : -1; };
+            auto ld_head = [&](int uu, unsigned long long& d, int& r0, int& r1) {
+                const int uc = uu >= 0 ? uu : 0;
+                const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                const int x0 = g.rowPtr[uc], x1 = g.rowPtr[uc + 1];
+                d = uu >= 0 ? d0 : INF_ENC;
+                r0 = uu >= 0 ? x0 : 0;
+                r1 = uu >= 0 ? x1 : 0;
+            };
+            auto ld_arc = [&](int a, int aEnd, int& c, double& w) {
+                const bool ok = a < aEnd;
+                const Arc A = g.arcs[ok ? a : 0];
+                c = ok ? A.col : -1;
+                w = A.lat;
+            };
+            int uC[BV], u1[BV], u2[BV], a0C[BV], a1C[BV], a01[BV], a11[BV], mcC[BV];
+            unsigned long long dbC[BV], db1[BV];
+            double mlC[BV];
+            {
+                const int i0 = take(), i1 = take(), i2 = take();
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    uC[v] = q_at(i0 + v);
+                    u1[v] = q_at(i1 + v);
+                    u2[v] = q_at(i2 + v);
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                ld_head(uC[v], dbC[v], a0C[v], a1C[v]);
+                ld_head(u1[v], db1[v], a01[v], a11[v]);
+            }
+#pragma unroll
+            for (int v = 0; v < BV; ++v) ld_arc(a0C[v] + l, a1C[v], mcC[v], mlC[v]);
+            while (uC[0] >= 0) {
+                int mc1[BV], a02[BV], a12[BV], u3[BV];
+                double ml1[BV];
+                unsigned long long db2[BV];
+#pragma unroll
+                for (int v = 0; v < BV; ++v) ld_arc(a01[v] + l, a11[v], mc1[v], ml1[v]);
+#pragma unroll
+                for (int v = 0; v < BV; ++v) ld_head(u2[v], db2[v], a02[v], a12[v]);
                 {
-                    const int i0 = take(), i1 = take(), i2 = take();
+                    const int i3 = take();
 #pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        uC[v] = q_at(i0 + v);
-                        u1[v] = q_at(i1 + v);
-                        u2[v] = q_at(i2 + v);
-                    }
+                    for (int v = 0; v < BV; ++v) u3[v] = q_at(i3 + v);
                 }
+                unsigned long long dub[BV];
+                int deg[BV], maxd = 0;
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    ld_head(uC[v], dbC[v], a0C[v], a1C[v]);
-                    ld_head(u1[v], db1[v], a01[v], a11[v]);
-                }
-#pragma unroll
-                for (int v = 0; v < BV; ++v) ld_arc(a0C[v] + l, a1C[v], mcC[v], mlC[v]);
-                while (uC[0] >= 0) {
-                    int mc1[BV], a02[BV], a12[BV], u3[BV];
-                    double ml1[BV];
-                    unsigned long long db2[BV];
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) ld_arc(a01[v] + l, a11[v], mc1[v], ml1[v]);
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) ld_head(u2[v], db2[v], a02[v], a12[v]);
-                    {
-                        const int i3 = take();
-#pragma unroll
-                        for (int v = 0; v < BV; ++v) u3[v] = q_at(i3 + v);
+                    const double k0 = b2d(dec(dbC[v])) + sh;
+                    const bool dirty = is_dirty(dbC[v]);
+                    const bool below = dirty && k0 < bound;
+                    const bool act = EAGER ? dirty && __ballot(below) >> gbase & LBMASK : below;
+                    const bool defer = dirty && !act;
+                    const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
+                    const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
+                    if (l == 0 && dmask) anyF.set(uC[v]);
+                    if (defer) {
+                        myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
+                        farAdd = 1;
                     }
-                    unsigned long long dub[BV];
-                    int deg[BV], maxd = 0;
+                    if (act) mark_clean(&D[(size_t)uC[v] * LB + l], dbC[v]);
+                    dub[v] = act ? dec(dbC[v]) : INF_BITS;
+                    deg[v] = amask ? a1C[v] - a0C[v] : 0;          // group-uniform
+                    if (amask && dbg && l == 0) {
+                        atomicAdd(&ctl->dProcs, 1u);
+                        atomicAdd(&ctl->dArcs, (unsigned int)deg[v]);
+                        atomicAdd(&ctl->dLanes, (unsigned int)__popc(amask));
+                    }
+                    maxd = max(maxd, deg[v]);
+                }
+                // relax the out-arcs for the dirty lanes below the bound
+                for (int c0 = 0; c0 < maxd; c0 += LB) {
+                    int mc[BV];
+                    double ml[BV];
 #pragma unroll
                     for (int v = 0; v < BV; ++v) {
-                        const double k0 = b2d(dec(dbC[v])) + sh;
-                        const bool dirty = is_dirty(dbC[v]);
-                        const bool below = dirty && k0 < bound;
-                        const bool act = EAGER ? dirty && __ballot(below) >> gbase & LBMASK : below;
-                        const bool defer = dirty && !act;
-                        const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
-                        const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                        if (l == 0 && dmask) anyF.set(uC[v]);
-                        if (defer) {
-                            myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
-                            farAdd = 1;
-                        }
-                        if (act) mark_clean(&D[(size_t)uC[v] * LB + l], dbC[v]);
-                        dub[v] = act ? dec(dbC[v]) : INF_BITS;
-                        deg[v] = amask ? a1C[v] - a0C[v] : 0;          // group-uniform
-                        if (amask && dbg && l == 0) {
-                            atomicAdd(&ctl->dProcs, 1u);
-                            atomicAdd(&ctl->dArcs, (unsigned int)deg[v]);
-                            atomicAdd(&ctl->dLanes, (unsigned int)__popc(amask));
-                        }
-                        maxd = max(maxd, deg[v]);
+                        mc[v] = mcC[v];
+                        ml[v] = mlC[v];
+                        if (c0 > 0) ld_arc(a0C[v] + c0 + l, a0C[v] + deg[v], mc[v], ml[v]);   // degree > LB
                     }
-                    // relax the out-arcs for the dirty lanes below the bound
-                    for (int c0 = 0; c0 < maxd; c0 += LB) {
-                        int mc[BV];
-                        double ml[BV];
-#pragma unroll
-                        for (int v = 0; v < BV; ++v) {
-                            mc[v] = mcC[v];
-                            ml[v] = mlC[v];
-                            if (c0 > 0) ld_arc(a0C[v] + c0 + l, a0C[v] + deg[v], mc[v], ml[v]);   // degree > LB
-                        }
-                        const int cn = min(LB, maxd - c0);
-                        for (int t = 0; t < cn; t += BKR) {
-                            int xs[BV][BKR];
-                            double ws[BV][BKR];
-                            unsigned long long dx[BV][BKR];
-#pragma unroll
-                            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                                for (int k = 0; k < BKR; ++k) {
-                                    const int srcL = gbase + min(t + k, LB - 1);   // inside the group
-                                    const int c = __shfl(mc[v], srcL, 64);
-                                    ws[v][k] = __shfl(ml[v], srcL, 64);
-                                    xs[v][k] = t + k < cn && c0 + t + k < deg[v] ? c : -1;   // (the chunk's own records)
-                                }
-#pragma unroll
-                            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                                for (int k = 0; k < BKR; ++k)
-                                    dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l);
-#pragma unroll
-                            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                                for (int k = 0; k < BKR; ++k) {
-                                    const int x = xs[v][k];
-                                    bool impN = false, impF = false;
-                                    if (x >= 0) {
-                                        const double nd = b2d(dub[v]) + ws[v][k];
-                                        const unsigned long long nb = d2b(nd);
-                                        if (nb < dec(dx[v][k])) {
-                                            relax_min(&D[(size_t)x * LB + l], enc_dirty(nb));
-                                            const double kx = nd + sh;
-                                            impN = kx < bound;
-                                            impF = !impN;
-                                            if (impF) myFar = d2b(kx) < myFar ? d2b(kx) : myFar;
-                                        }
-                                    }
-                                    const uint64_t bn = __ballot(impN), bf = __ballot(impF);
-                                    if (l == 0) {
-                                        if ((bn >> gbase) & LBMASK) anyC.set(x);
-                                        if ((bf >> gbase) & LBMASK) {
-                                            anyF.set(x);
-                                            farAdd = 1;
-                                        }
-                                    }
-                                }
-                        }
-                    }
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        uC[v] = u1[v]; dbC[v] = db1[v]; a0C[v] = a01[v]; a1C[v] = a11[v];
-                        mcC[v] = mc1[v]; mlC[v] = ml1[v];
-                        u1[v] = u2[v]; db1[v] = db2[v]; a01[v] = a02[v]; a11[v] = a12[v];
-                        u2[v] = u3[v];
-                    }
-                }
-            } else {
-                int i0 = take();
-                int u[BV], a0[BV], a1[BV];
-                unsigned long long db[BV];
-#pragma unroll
-                for (int v = 0; v < BV; ++v) u[v] = i0 + v < qn ? ld_wg(&Q[min(i0 + v, qc)]) : -1;
-#pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    // branch-free: one round trip for dist[u] and rowPtr[u..u+1]
-                    const int uc = u[v] >= 0 ? u[v] : 0;
-                    const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
-                    const int r0 = g.rowPtr[uc], r1 = g.rowPtr[uc + 1];
-                    db[v] = u[v] >= 0 ? d0 : INF_ENC;
-                    a0[v] = u[v] >= 0 ? r0 : 0;
-                    a1[v] = u[v] >= 0 ? r1 : 0;
-                }
-                int i1 = take();
-                int nq[BV];
-#pragma unroll
-                for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i1 + v, qc)]);
-                while (i0 < qn) {
-                    int un[BV], a0n[BV], a1n[BV];
-                    unsigned long long dbn[BV], dub[BV];
-                    auto fetch_next = [&]() {
-#pragma unroll
-                        for (int v = 0; v < BV; ++v) {
-                            const int uc = un[v] >= 0 ? un[v] : 0;
-                            dbn[v] = ld_wg(&D[(size_t)uc * LB + l]);
-                            a0n[v] = g.rowPtr[uc];
-                            a1n[v] = g.rowPtr[uc + 1];
-                        }
-                    };
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) un[v] = i1 + v < qn ? nq[v] : -1;
-                    if constexpr (PIPE) fetch_next();
-                    const int i2 = take();
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) nq[v] = ld_wg(&Q[min(i2 + v, qc)]);
-                    int maxd = 0;
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        const double k0 = b2d(dec(db[v])) + sh;
-                        const bool dirty = is_dirty(db[v]);
-                        const bool below = dirty && k0 < bound;
-                        const bool act = EAGER ? dirty && __ballot(below) >> gbase & LBMASK : below;
-                        const bool defer = dirty && !act;
-                        const uint32_t amask = (uint32_t)(__ballot(act) >> gbase) & LBMASK;
-                        const uint32_t dmask = (uint32_t)(__ballot(defer) >> gbase) & LBMASK;
-                        if (l == 0 && dmask) anyF.set(u[v]);
-                        if (defer) {
-                            myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
-                            farAdd = 1;
-                        }
-                        if (act) mark_clean(&D[(size_t)u[v] * LB + l], db[v]);
-                        dub[v] = act ? dec(db[v]) : INF_BITS;
-                        if (!amask) a1[v] = a0[v];
-                        else if (dbg && l == 0) {
-                            atomicAdd(&ctl->dProcs, 1u);
-                            atomicAdd(&ctl->dArcs, (unsigned int)(a1[v] - a0[v]));
-                            atomicAdd(&ctl->dLanes, (unsigned int)__popc(amask));
-                        }
-                        maxd = max(maxd, a1[v] - a0[v]);
-                    }
-                    // relax u's out-arcs for the dirty lanes below the bound
-                    for (int t = 0; t < maxd; t += BK) {
-                        int xs[BV][BK];
-                        double ws[BV][BK];
-                        unsigned long long dx[BV][BK];
-                        // branch-free: out-of-range slots load arc 0 / vertex 0
-                        // and are masked, so all BV*BK loads of a stage are in
-                        // flight before the first wait
+                    const int cn = min(LB, maxd - c0);
+                    for (int t = 0; t < cn; t += BKR) {
+                        int xs[BV][BKR];
+                        double ws[BV][BKR];
+                        unsigned long long dx[BV][BKR];
 #pragma unroll
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
-                            for (int k = 0; k < BK; ++k) {
-                                const int a = a0[v] + t + k;
-                                const bool ok = a < a1[v];
-                                const Arc A = g.arcs[ok ? a : 0];
-                                xs[v][k] = ok ? A.col : -1;
-                                ws[v][k] = A.lat;
+                            for (int k = 0; k < BKR; ++k) {
+                                const int srcL = gbase + min(t + k, LB - 1);   // inside the group
+                                const int c = __shfl(mc[v], srcL, 64);
+                                ws[v][k] = __shfl(ml[v], srcL, 64);
+                                xs[v][k] = t + k < cn && c0 + t + k < deg[v] ? c : -1;   // (the chunk's own records)
                             }
 #pragma unroll
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
-                            for (int k = 0; k < BK; ++k)
+                            for (int k = 0; k < BKR; ++k)
                                 dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l);
 #pragma unroll
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
-                            for (int k = 0; k < BK; ++k) {
+                            for (int k = 0; k < BKR; ++k) {
                                 const int x = xs[v][k];
                                 bool impN = false, impF = false;
                                 if (x >= 0) {
@@ -770,16 +632,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 }
                             }
                     }
-                    if constexpr (!PIPE) fetch_next();
-                    i0 = i1;
-                    i1 = i2;
+                }
 #pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        u[v] = un[v];
-                        db[v] = un[v] >= 0 ? dbn[v] : INF_ENC;
-                        a0[v] = un[v] >= 0 ? a0n[v] : 0;
-                        a1[v] = un[v] >= 0 ? a1n[v] : 0;
-                    }
+                for (int v = 0; v < BV; ++v) {
+                    uC[v] = u1[v]; dbC[v] = db1[v]; a0C[v] = a01[v]; a1C[v] = a11[v];
+                    mcC[v] = mc1[v]; mlC[v] = ml1[v];
+                    u1[v] = u2[v]; db1[v] = db2[v]; a01[v] = a02[v]; a11[v] = a12[v];
+                    u2[v] = u3[v];
                 }
             }
             if (dbg && l == 0) {
@@ -836,257 +695,105 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 __syncthreads();
             }
             while (lo < hi) {
-            if constexpr (PIPE) {
-                // the relax loop's three-stage pipeline (BV list entries per
-                // group and stride): the group's lanes hold one in-arc record
-                // per entry (lane l: in-arc a0 + l, one coalesced read), the
-                // scan takes the tails by cross-lane reads, so an entry's
-                // chain is its BKQ-wide dist gathers.  Records of the next
-                // stride, dist lines + in-arc ranges of the one after, list
-                // entries of the third are in flight meanwhile.
-                const int S = NG * BV;
-                auto item = [&](int i) { return i < hi ? (fullPred ? i : ld_wg(&Q[i])) : -1; };
-                auto ld_head = [&](int vv, unsigned long long& d, int& r0, int& r1) {
-                    const int vc = vv >= 0 ? vv : 0;
-                    const unsigned long long d0 = dec(ld_wg(&D[(size_t)vc * LB + l]));
-                    const int x0 = undirected ? g.rowPtr[vc] : g.inPtr[vc];
-                    const int x1 = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
-                    d = vv >= 0 ? d0 : INF_BITS;
-                    r0 = vv >= 0 ? x0 : 0;
-                    r1 = vv >= 0 ? x1 : 0;
-                };
-                auto ld_rec = [&](int a, int aEnd, int& c, double& w) {
-                    const bool ok = a < aEnd;
-                    const int ac = ok ? a : 0;
-                    if (undirected) {
-                        const Arc A = g.arcs[ac];
-                        c = A.col;
-                        w = A.lat;
-                    } else {
-                        c = g.inCol[ac];
-                        w = g.inLat[ac];
-                    }
-                    c = ok ? c : -1;
-                };
-                int v0 = lo + gid * BV;
-                int vC[BV], v1[BV], v2[BV], a0C[BV], a1C[BV], a01[BV], a11[BV], mcC[BV];
-                unsigned long long dC[BV], d1[BV];
-                double mlC[BV];
+            // the relax loop's three-stage pipeline (BV list entries per
+            // group and stride): the group's lanes hold one in-arc record
+            // per entry (lane l: in-arc a0 + l, one coalesced read), the
+            // scan takes the tails by cross-lane reads, so an entry's
+            // chain is its BKQ-wide dist gathers.  Records of the next
+            // stride, dist lines + in-arc ranges of the one after, list
+            // entries of the third are in flight meanwhile.
+            const int S = NG * BV;
+            auto item = [&](int i) { return i < hi ? (fullPred ? i : ld_wg(&Q[i])) : -1; };
+            auto ld_head = [&](int vv, unsigned long long& d, int& r0, int& r1) {
+                const int vc = vv >= 0 ? vv : 0;
+                const unsigned long long d0 = dec(ld_wg(&D[(size_t)vc * LB + l]));
+                const int x0 = undirected ? g.rowPtr[vc] : g.inPtr[vc];
+                const int x1 = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
+                d = vv >= 0 ? d0 : INF_BITS;
+                r0 = vv >= 0 ? x0 : 0;
+                r1 = vv >= 0 ? x1 : 0;
+            };
+            auto ld_rec = [&](int a, int aEnd, int& c, double& w) {
+                const bool ok = a < aEnd;
+                const int ac = ok ? a : 0;
+                if (undirected) {
+                    const Arc A = g.arcs[ac];
+                    c = A.col;
+                    w = A.lat;
+                } else {
+                    c = g.inCol[ac];
+                    w = g.inLat[ac];
+                }
+                c = ok ? c : -1;
+            };
+            int v0 = lo + gid * BV;
+            int vC[BV], v1[BV], v2[BV], a0C[BV], a1C[BV], a01[BV], a11[BV], mcC[BV];
+            unsigned long long dC[BV], d1[BV];
+            double mlC[BV];
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                vC[v] = item(v0 + v);
+                v1[v] = item(v0 + S + v);
+                v2[v] = item(v0 + 2 * S + v);
+            }
+#pragma unroll
+            for (int v = 0; v < BV; ++v) {
+                ld_head(vC[v], dC[v], a0C[v], a1C[v]);
+                ld_head(v1[v], d1[v], a01[v], a11[v]);
+            }
+#pragma unroll
+            for (int v = 0; v < BV; ++v) ld_rec(a0C[v] + l, a1C[v], mcC[v], mlC[v]);
+            for (; v0 < hi; v0 += S) {
+                int mc1[BV], a02[BV], a12[BV], v3[BV];
+                double ml1[BV];
+                unsigned long long d2[BV];
+#pragma unroll
+                for (int v = 0; v < BV; ++v) ld_rec(a01[v] + l, a11[v], mc1[v], ml1[v]);
+#pragma unroll
+                for (int v = 0; v < BV; ++v) ld_head(v2[v], d2[v], a02[v], a12[v]);
+#pragma unroll
+                for (int v = 0; v < BV; ++v) v3[v] = item(v0 + 3 * S + v);
+                bool root[BV];
+                unsigned long long best[BV], mn[BV];
+                int cnt[BV], ba[BV], bu[BV], deg[BV], maxd = 0;
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
-                    vC[v] = item(v0 + v);
-                    v1[v] = item(v0 + S + v);
-                    v2[v] = item(v0 + 2 * S + v);
+                    root[v] = vC[v] == src || src < 0;
+                    best[v] = INF_BITS;
+                    mn[v] = INF_BITS;
+                    cnt[v] = 0;
+                    ba[v] = -1;
+                    bu[v] = -1;
+                    deg[v] = vC[v] >= 0 ? a1C[v] - a0C[v] : 0;   // group-uniform
+                    maxd = max(maxd, deg[v]);
                 }
-#pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    ld_head(vC[v], dC[v], a0C[v], a1C[v]);
-                    ld_head(v1[v], d1[v], a01[v], a11[v]);
-                }
-#pragma unroll
-                for (int v = 0; v < BV; ++v) ld_rec(a0C[v] + l, a1C[v], mcC[v], mlC[v]);
-                for (; v0 < hi; v0 += S) {
-                    int mc1[BV], a02[BV], a12[BV], v3[BV];
-                    double ml1[BV];
-                    unsigned long long d2[BV];
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) ld_rec(a01[v] + l, a11[v], mc1[v], ml1[v]);
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) ld_head(v2[v], d2[v], a02[v], a12[v]);
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) v3[v] = item(v0 + 3 * S + v);
-                    bool root[BV];
-                    unsigned long long best[BV], mn[BV];
-                    int cnt[BV], ba[BV], bu[BV], deg[BV], maxd = 0;
+                for (int c0 = 0; c0 < maxd; c0 += LB) {
+                    int mc[BV];
+                    double ml[BV];
 #pragma unroll
                     for (int v = 0; v < BV; ++v) {
-                        root[v] = vC[v] == src || src < 0;
-                        best[v] = INF_BITS;
-                        mn[v] = INF_BITS;
-                        cnt[v] = 0;
-                        ba[v] = -1;
-                        bu[v] = -1;
-                        deg[v] = vC[v] >= 0 ? a1C[v] - a0C[v] : 0;   // group-uniform
-                        maxd = max(maxd, deg[v]);
+                        mc[v] = mcC[v];
+                        ml[v] = mlC[v];
+                        if (c0 > 0) ld_rec(a0C[v] + c0 + l, a0C[v] + deg[v], mc[v], ml[v]);
                     }
-                    for (int c0 = 0; c0 < maxd; c0 += LB) {
-                        int mc[BV];
-                        double ml[BV];
-#pragma unroll
-                        for (int v = 0; v < BV; ++v) {
-                            mc[v] = mcC[v];
-                            ml[v] = mlC[v];
-                            if (c0 > 0) ld_rec(a0C[v] + c0 + l, a0C[v] + deg[v], mc[v], ml[v]);
-                        }
-                        const int cn = min(LB, maxd - c0);
-                        for (int t = 0; t < cn; t += BKQ) {
-                            int cu[BV][BKQ];
-                            double lw[BV][BKQ];
-                            unsigned long long du[BV][BKQ];
-#pragma unroll
-                            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                                for (int k = 0; k < BKQ; ++k) {
-                                    const int srcL = gbase + min(t + k, LB - 1);
-                                    const int c = __shfl(mc[v], srcL, 64);
-                                    lw[v][k] = __shfl(ml[v], srcL, 64);
-                                    cu[v][k] = t + k < cn && c0 + t + k < deg[v] ? c : -1;   // (a repeat would count as a tie)
-                                }
-#pragma unroll
-                            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                                for (int k = 0; k < BKQ; ++k) {
-                                    const unsigned long long t2 =
-                                        dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]));
-                                    du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
-                                }
-#pragma unroll
-                            for (int v = 0; v < BV; ++v)
-#pragma unroll
-                                for (int k = 0; k < BKQ; ++k) {
-                                    if (cu[v][k] < 0 || root[v]) continue;
-                                    const double cand = b2d(du[v][k]) + lw[v][k];
-                                    const unsigned long long cb = d2b(cand);
-                                    mn[v] = cb < mn[v] ? cb : mn[v];
-                                    if (dC[v] != INF_BITS && du[v][k] <= dC[v] && cand == b2d(dC[v])) {
-                                        if (du[v][k] < best[v]) {
-                                            best[v] = du[v][k];
-                                            cnt[v] = 1;
-                                            ba[v] = a0C[v] + c0 + t + k;
-                                            bu[v] = cu[v][k];
-                                        } else if (du[v][k] == best[v]) {
-                                            ++cnt[v];
-                                        }
-                                    }
-                                }
-                        }
-                    }
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        const int vv = vC[v];
-                        if (vv < 0) continue;
-                        const size_t e = (size_t)vv * LB + l;
-                        const bool bad = !root[v] && mn[v] < dC[v];
-                        if (bad) {
-                            D[e] = enc_dirty(mn[v]);
-                            viol = 1;
-                        }
-                        const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
-                        if (bm && l == 0) anyC.set(vv);
-                        const bool tree = !root[v] && dC[v] != INF_BITS && ba[v] >= 0;
-                        // ambiguous (see the generic loop below)
-                        const bool ea = !root[v] && dC[v] != INF_BITS && (cnt[v] != 1 || best[v] == dC[v]);
-                        const int hx = tree ? ba[v] : -1;
-                        P[e] = ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx;
-                        const bool isSrc = vv == src;
-                        H[e] = isSrc ? 0 : -1;
-                        R[e] = isSrc ? 1.0 : -1.0;
-                        if (!tree) bu[v] = -1;
-                    }
-                    if (!fullPred) {
-#pragma unroll
-                        for (int v = 0; v < BV; ++v) {
-                            const int p = vC[v] >= 0 ? bu[v] : -1;
-                            wave_append(Q, &ctl->qtail, p >= 0 && !clm.test_set(p), p);
-                        }
-                    }
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        vC[v] = v1[v]; dC[v] = d1[v]; a0C[v] = a01[v]; a1C[v] = a11[v];
-                        mcC[v] = mc1[v]; mlC[v] = ml1[v];
-                        v1[v] = v2[v]; d1[v] = d2[v]; a01[v] = a02[v]; a11[v] = a12[v];
-                        v2[v] = v3[v];
-                    }
-                }
-            } else {
-                // software-pipelined like the relax's light loop: the next
-                // stride's dist lines and in-arc ranges are in flight while this
-                // stride scans its in-arcs, the list entries one stride further
-                const int S = NG * BV;
-                int v0 = lo + gid * BV;
-                int vx[BV], a0[BV], a1[BV], qv[BV];
-                unsigned long long dvb[BV];
-#pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    const int i = v0 + v;
-                    vx[v] = i < hi ? (fullPred ? i : ld_wg(&Q[i])) : -1;
-                }
-#pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    const int vc = vx[v] >= 0 ? vx[v] : 0;
-                    const unsigned long long d0 = dec(ld_wg(&D[(size_t)vc * LB + l]));
-                    const int r0 = undirected ? g.rowPtr[vc] : g.inPtr[vc];
-                    const int r1 = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
-                    dvb[v] = vx[v] >= 0 ? d0 : INF_BITS;
-                    a0[v] = vx[v] >= 0 ? r0 : 0;
-                    a1[v] = vx[v] >= 0 ? r1 : 0;
-                }
-#pragma unroll
-                for (int v = 0; v < BV; ++v) {
-                    const int i = v0 + S + v;
-                    qv[v] = fullPred ? i : ld_wg(&Q[min(i, hi - 1)]);
-                }
-                for (; v0 < hi; v0 += S) {
-                    int vxn[BV], a0n[BV], a1n[BV];
-                    unsigned long long dvn[BV];
-                    auto fetch_next = [&]() {
-#pragma unroll
-                        for (int v = 0; v < BV; ++v) {
-                            const int vc = vxn[v] >= 0 ? vxn[v] : 0;
-                            dvn[v] = ld_wg(&D[(size_t)vc * LB + l]);
-                            a0n[v] = undirected ? g.rowPtr[vc] : g.inPtr[vc];
-                            a1n[v] = undirected ? g.rowPtr[vc + 1] : g.inPtr[vc + 1];
-                        }
-                    };
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) vxn[v] = v0 + S + v < hi ? qv[v] : -1;
-                    if constexpr (PIPE) fetch_next();
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        const int i = v0 + 2 * S + v;
-                        qv[v] = fullPred ? i : ld_wg(&Q[min(i, hi - 1)]);
-                    }
-                    int ba[BV], cnt[BV], bu[BV];
-                    unsigned long long best[BV], mn[BV];
-                    bool root[BV];
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        root[v] = vx[v] == src || src < 0;
-                        best[v] = INF_BITS;
-                        mn[v] = INF_BITS;
-                        cnt[v] = 0;
-                        ba[v] = -1;
-                        bu[v] = -1;
-                    }
-                    int maxd = 0;
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) maxd = max(maxd, a1[v] - a0[v]);
-                    for (int t = 0; t < maxd; t += BKP) {
-                        int cu[BV][BKP];
-                        double lw[BV][BKP];
-                        unsigned long long du[BV][BKP];
+                    const int cn = min(LB, maxd - c0);
+                    for (int t = 0; t < cn; t += BKQ) {
+                        int cu[BV][BKQ];
+                        double lw[BV][BKQ];
+                        unsigned long long du[BV][BKQ];
 #pragma unroll
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
-                            for (int k = 0; k < BKP; ++k) {      // branch-free (see pass 1)
-                                const int a = a0[v] + t + k;
-                                const bool ok = a < a1[v];
-                                const int ac = ok ? a : 0;
-                                int c;
-                                if (undirected) {
-                                    const Arc A = g.arcs[ac];
-                                    c = A.col;
-                                    lw[v][k] = A.lat;
-                                } else {
-                                    c = g.inCol[ac];
-                                    lw[v][k] = g.inLat[ac];
-                                }
-                                cu[v][k] = ok ? c : -1;
+                            for (int k = 0; k < BKQ; ++k) {
+                                const int srcL = gbase + min(t + k, LB - 1);
+                                const int c = __shfl(mc[v], srcL, 64);
+                                lw[v][k] = __shfl(ml[v], srcL, 64);
+                                cu[v][k] = t + k < cn && c0 + t + k < deg[v] ? c : -1;   // (a repeat would count as a tie)
                             }
 #pragma unroll
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
-                            for (int k = 0; k < BKP; ++k) {
+                            for (int k = 0; k < BKQ; ++k) {
                                 const unsigned long long t2 =
                                     dec(ld_wg(&D[(size_t)(cu[v][k] >= 0 ? cu[v][k] : 0) * LB + l]));
                                 du[v][k] = cu[v][k] >= 0 ? t2 : INF_BITS;
@@ -1094,16 +801,16 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
-                            for (int k = 0; k < BKP; ++k) {
+                            for (int k = 0; k < BKQ; ++k) {
                                 if (cu[v][k] < 0 || root[v]) continue;
                                 const double cand = b2d(du[v][k]) + lw[v][k];
                                 const unsigned long long cb = d2b(cand);
                                 mn[v] = cb < mn[v] ? cb : mn[v];
-                                if (dvb[v] != INF_BITS && du[v][k] <= dvb[v] && cand == b2d(dvb[v])) {
+                                if (dC[v] != INF_BITS && du[v][k] <= dC[v] && cand == b2d(dC[v])) {
                                     if (du[v][k] < best[v]) {
                                         best[v] = du[v][k];
                                         cnt[v] = 1;
-                                        ba[v] = a0[v] + t + k;
+                                        ba[v] = a0C[v] + c0 + t + k;
                                         bu[v] = cu[v][k];
                                     } else if (du[v][k] == best[v]) {
                                         ++cnt[v];
@@ -1111,54 +818,42 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 }
                             }
                     }
+                }
+#pragma unroll
+                for (int v = 0; v < BV; ++v) {
+                    const int vv = vC[v];
+                    if (vv < 0) continue;
+                    const size_t e = (size_t)vv * LB + l;
+                    const bool bad = !root[v] && mn[v] < dC[v];
+                    if (bad) {
+                        D[e] = enc_dirty(mn[v]);
+                        viol = 1;
+                    }
+                    const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
+                    if (bm && l == 0) anyC.set(vv);
+                    const bool tree = !root[v] && dC[v] != INF_BITS && ba[v] >= 0;
+                    // ambiguous (see the generic loop below)
+                    const bool ea = !root[v] && dC[v] != INF_BITS && (cnt[v] != 1 || best[v] == dC[v]);
+                    const int hx = tree ? ba[v] : -1;
+                    P[e] = ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx;
+                    const bool isSrc = vv == src;
+                    H[e] = isSrc ? 0 : -1;
+                    R[e] = isSrc ? 1.0 : -1.0;
+                    if (!tree) bu[v] = -1;
+                }
+                if (!fullPred) {
 #pragma unroll
                     for (int v = 0; v < BV; ++v) {
-                        const int vv = vx[v];
-                        if (vv < 0) continue;
-                        const size_t e = (size_t)vv * LB + l;
-                        const bool bad = !root[v] && mn[v] < dvb[v];
-                        if (bad) {
-                            D[(size_t)vv * LB + l] = enc_dirty(mn[v]);
-                            viol = 1;
-                        }
-                        const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
-                        if (bm && l == 0) anyC.set(vv);
-                        const bool tree = !root[v] && dvb[v] != INF_BITS && ba[v] >= 0;
-                        // an entry whose parent the heap decides: equal minimum
-                        // tight predecessors, or the minimum one reaches v by a
-                        // zero-increment arc (dist[u] + w == dist[u]: u and v
-                        // share a key).  A zero-increment arc from a farther
-                        // predecessor cannot win (its relaxation is not strictly
-                        // better).  Marked in H (free until the hop counts) for
-                        // the tie export below.
-                        const bool ea = !root[v] && dvb[v] != INF_BITS &&
-                                        (cnt[v] != 1 || best[v] == dvb[v]);
-                        // P: the tree IN-arc, TIE_AMB marking an entry whose
-                        // parent the heap decides; labels unresolved (-1) except
-                        // at the source (hops 0, rel 1: the fold's start)
-                        const int hx = tree ? ba[v] : -1;
-                        P[e] = ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx;
-                        const bool isSrc = vv == src;
-                        H[e] = isSrc ? 0 : -1;
-                        R[e] = isSrc ? 1.0 : -1.0;
-                        if (!tree) bu[v] = -1;
+                        const int p = vC[v] >= 0 ? bu[v] : -1;
+                        wave_append(Q, &ctl->qtail, p >= 0 && !clm.test_set(p), p);
                     }
-                    if (!fullPred) {
-                        // claim and list the parents (next round)
+                }
 #pragma unroll
-                        for (int v = 0; v < BV; ++v) {
-                            const int p = vx[v] >= 0 ? bu[v] : -1;
-                            wave_append(Q, &ctl->qtail, p >= 0 && !clm.test_set(p), p);
-                        }
-                    }
-                    if constexpr (!PIPE) fetch_next();
-#pragma unroll
-                    for (int v = 0; v < BV; ++v) {
-                        vx[v] = vxn[v];
-                        dvb[v] = vxn[v] >= 0 ? dec(dvn[v]) : INF_BITS;
-                        a0[v] = vxn[v] >= 0 ? a0n[v] : 0;
-                        a1[v] = vxn[v] >= 0 ? a1n[v] : 0;
-                    }
+                for (int v = 0; v < BV; ++v) {
+                    vC[v] = v1[v]; dC[v] = d1[v]; a0C[v] = a01[v]; a1C[v] = a11[v];
+                    mcC[v] = mc1[v]; mlC[v] = ml1[v];
+                    v1[v] = v2[v]; d1[v] = d2[v]; a01[v] = a02[v]; a11[v] = a12[v];
+                    v2[v] = v3[v];
                 }
             }
             if (fullPred) break;
