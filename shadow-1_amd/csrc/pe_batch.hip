@@ -177,6 +177,29 @@ __device__ __forceinline__ void st_wg(int32_t* p, int v) {
 __device__ __forceinline__ void st_wg(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+__device__ __forceinline__ void st_wg(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// label records (BLabel): two 8-B halves of one 16-B slot, loaded / stored
+// with relaxed workgroup-scope accesses (walks of other groups race on them:
+// a half-written record reads as unresolved -- hop label -1 or rel < 0 --
+// and the reader walks on, as the labels are written once with the only
+// value the fold can give)
+struct Lbl {
+    double rel;
+    int hops, arc;
+};
+__device__ __forceinline__ Lbl lbl_ld(BLabel* p) {
+    const unsigned long long x = ld_wg(&p->ha);
+    return Lbl{ld_wg(&p->rel), (int)(unsigned)x, (int)(unsigned)(x >> 32)};
+}
+__device__ __forceinline__ int lbl_arc(BLabel* p) { return (int)(unsigned)(ld_wg(&p->ha) >> 32); }
+__device__ __forceinline__ void lbl_st(BLabel* p, double rel, int hops, int arc) {
+    st_wg(&p->rel, rel);
+    st_wg(&p->ha, (unsigned long long)(unsigned)hops | ((unsigned long long)(unsigned)arc << 32));
+}
+__device__ __forceinline__ bool lbl_known(const Lbl& x) { return x.hops >= 0 && x.rel >= 0.0; }
 
 // Forward reliability fold with vertex factors (topology.c:1430-1462, :1499)
 // along lane l's predecessor chain, multiplied in source -> target order:
@@ -186,18 +209,18 @@ template <int LB>
 __device__ __noinline__ double fold_rel_batch(const double* __restrict__ vrel,
                                               const double* __restrict__ inRel,
                                               const int32_t* __restrict__ inCol,
-                                              const int32_t* P, int l, int s, int t, int h) {
+                                              BLabel* LBL, int l, int s, int t, int h) {
     // (arrays by value: a DevGraph& would pin the caller's descriptor in scratch)
     double acc = 1.0 * vrel[s];
     acc = acc * vrel[t];
     for (int lo = 0; lo < h; lo += 64) {        // hops (lo, hi] counted from the source
         const int hi = min(h, lo + 64);
         int x = t;
-        for (int up = 0; up < h - hi; ++up) x = inCol[ld_wg(&P[(size_t)x * LB + l]) & ~TIE_AMB];
+        for (int up = 0; up < h - hi; ++up) x = inCol[lbl_arc(&LBL[(size_t)x * LB + l]) & ~TIE_AMB];
         double fac[64];
         int k = 0;
         while (k < hi - lo) {
-            const int a = ld_wg(&P[(size_t)x * LB + l]) & ~TIE_AMB;
+            const int a = lbl_arc(&LBL[(size_t)x * LB + l]) & ~TIE_AMB;
             fac[k++] = inRel[a];
             x = inCol[a];
         }
@@ -255,9 +278,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const size_t NS = (size_t)bs.nStride;
     const size_t SE = NS * LB;
     unsigned long long* D = as_global(bs.D + slot * SE);
-    double* R = as_global(bs.R + slot * SE);
-    int32_t* H = as_global(bs.H + slot * SE);
-    int32_t* P = as_global(bs.P + slot * SE);
+    BLabel* LBL = as_global(bs.L + slot * SE);
     int32_t* Q = as_global(bs.queue + slot * NS);
 
     // batches are taken from a device counter (dynamic: a batch's cost varies
@@ -302,7 +323,6 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
         if (PT != 2 && gid == 0 && src >= 0) {
             D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
-            R[(size_t)src * LB + l] = 1.0;
             any0.set(src);
         }
         fence_wg();
@@ -835,10 +855,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     // ambiguous (see the generic loop below)
                     const bool ea = !root[v] && dC[v] != INF_BITS && (cnt[v] != 1 || best[v] == dC[v]);
                     const int hx = tree ? ba[v] : -1;
-                    P[e] = ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx;
                     const bool isSrc = vv == src;
-                    H[e] = isSrc ? 0 : -1;
-                    R[e] = isSrc ? 1.0 : -1.0;
+                    lbl_st(&LBL[e], isSrc ? 1.0 : -1.0, isSrc ? 0 : -1,
+                           ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx);
                     if (!tree) bu[v] = -1;
                 }
                 if (!fullPred) {
@@ -926,16 +945,19 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     const size_t e = (size_t)t * LB + l;
                     const unsigned long long dt = dec(ld_wg(&D[(size_t)t * LB + l]));
                     if (dt != INF_BITS) {
-                        int he = ld_wg(&H[e]);
-                        double re = ld_wg(&R[e]);
+                        // one record per step: an entry's record holds its
+                        // parent arc, the parent's record its labels and the
+                        // next arc up
+                        Lbl cr = lbl_ld(&LBL[e]);
                         int steps = 0;
                         int cur = (int)e;
-                        while (!(he >= 0 && re >= 0.0)) {
+                        while (!lbl_known(cr)) {
                             int sp = 0, x = cur, hp = 0;
+                            Lbl xr = cr;
                             double rp = 0.0;
                             bool found = false;
                             while (sp < SMAX) {
-                                const int a = ld_wg(&P[x]);
+                                const int a = xr.arc;
                                 if (a < 0 || ++steps > stepCap) {
                                     if (a >= 0 && pass == 0) deep = true;   // -> sweeps
                                     else relAmb = 1u;      // no parent / a cycle: exact path
@@ -944,38 +966,34 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                     break;
                                 }
                                 relAmb |= (uint32_t)((a & TIE_AMB) != 0);
-                                const int arc = a & ~TIE_AMB;
-                                stk[sp * NT + tid] = make_int2(x, arc);
+                                stk[sp * NT + tid] = make_int2(x, a);
                                 ++sp;
-                                const int pe = g.inCol[arc] * LB + l;
-                                const int hq = ld_wg(&H[pe]);
-                                const double rq = ld_wg(&R[pe]);
-                                if (hq >= 0 && rq >= 0.0) {
-                                    hp = hq;
-                                    rp = rq;
+                                const int pe = g.inCol[a & ~TIE_AMB] * LB + l;
+                                const Lbl pr = lbl_ld(&LBL[pe]);
+                                if (lbl_known(pr)) {
+                                    hp = pr.hops;
+                                    rp = pr.rel;
                                     found = true;
                                     break;
                                 }
                                 x = pe;
+                                xr = pr;
                             }
                             if (!found) {           // chain longer than SMAX: its top first
                                 cur = x;
+                                cr = xr;
                                 continue;
                             }
                             for (int i = sp - 1; i >= 0; --i) {
                                 const int2 sx = stk[i * NT + tid];
                                 hp += 1;
-                                rp = rp * g.inRel[sx.y];
-                                st_wg(&H[sx.x], hp);
-                                st_wg(&R[sx.x], rp);
+                                rp = rp * g.inRel[sx.y & ~TIE_AMB];
+                                lbl_st(&LBL[sx.x], rp, hp, sx.y);
                             }
                             if (sp == 0) break;     // gave up (deep / inconsistent)
-                            if (cur == (int)e) {
-                                he = hp;
-                                re = rp;
-                                break;
-                            }
+                            if (cur == (int)e) break;
                             cur = (int)e;           // top segment resolved: walk again
+                            cr = lbl_ld(&LBL[e]);
                         }
                     }
                 }
@@ -1001,19 +1019,18 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         for (int sweep = 0; sweep <= n + 1; ++sweep) {
             int ch = 0;
             for (size_t e = tid; e < NE; e += NT) {
-                const int a = ld_wg(&P[e]);
+                const Lbl er = lbl_ld(&LBL[e]);
+                const int a = er.arc;
                 if (a < 0) continue;
                 const int ll = (int)(e % LB);
                 const int arc = a & ~TIE_AMB;
                 const int pe = g.inCol[arc] * LB + ll;
-                const int hq = ld_wg(&H[pe]);
-                const double rq = ld_wg(&R[pe]);
-                if (hq < 0 || rq < 0.0) continue;
-                const int hn = hq + 1;
-                const double rn = rq * g.inRel[arc];
-                if (ld_wg(&H[e]) != hn || ld_wg(&R[e]) != rn) {
-                    st_wg(&H[e], hn);
-                    st_wg(&R[e], rn);
+                const Lbl pr = lbl_ld(&LBL[pe]);
+                if (!lbl_known(pr)) continue;
+                const int hn = pr.hops + 1;
+                const double rn = pr.rel * g.inRel[arc];
+                if (er.hops != hn || er.rel != rn) {
+                    lbl_st(&LBL[e], rn, hn, a);
                     ch = 1;
                     if (a & TIE_AMB) atomicOr(&ctl->ambMask, 1u << ll);
                 }
@@ -1069,14 +1086,15 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             f |= F_UNREACHABLE;
                         } else {
                             L = b2d(dt);
-                            h = ld_wg(&H[e]);
-                            const int pa = ld_wg(&P[e]);
+                            const Lbl er = lbl_ld(&LBL[e]);
+                            h = er.hops;
+                            const int pa = er.arc;
                             pv = pa >= 0 ? g.inCol[pa & ~TIE_AMB] : -1;
                             if (pv >= 0 && g.oldId) pv = g.oldId[pv];   // device id -> caller's id
                             if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
-                                Rl = ld_wg(&R[e]);
+                                Rl = er.rel;
                             else
-                                Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, P, l, src, t, h);
+                                Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, LBL, l, src, t, h);
                             if (L == 0.0) {                 // topology.c:1848-1852
                                 L = 1.0;
                                 f |= F_ZEROLAT;
@@ -1153,7 +1171,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             for (int v = gid; v < n; v += NG) {
                 if (sl < 0) continue;
                 const size_t e = (size_t)v * LB + l;
-                const int pe = ld_wg(&P[e]);
+                const int pe = lbl_arc(&LBL[e]);
                 const bool am = pe >= 0 && (pe & TIE_AMB);
                 const size_t o = (size_t)sl * (size_t)tie.n + v;
                 tie.D[o] = b2d(dec(ld_wg(&D[(size_t)v * LB + l])));

@@ -108,11 +108,18 @@ struct DevScratch {
 // workgroup; every per-vertex array is [n][LB] (LB sources of the batch
 // side by side, so one arc relaxation serves LB sources with one coalesced
 // access).
+// Per (vertex, lane) labels of the post kernel, one 16-B record: the label
+// walks read a parent's reliability, hop count AND its own parent arc with
+// one access instead of three (round 5).
+struct alignas(16) BLabel {
+    double rel;              // reliability product label (< 0 unresolved)
+    unsigned long long ha;   // hop label (low 32 bits, -1 unresolved) | chosen IN-arc << 32
+                             // (| TIE_AMB; -1 none)
+};
+
 struct BatchScratch {
     unsigned long long* D;   // [slot][nStride][LB] f64 bit patterns (dist)
-    double* R;               // [slot][nStride][LB] rel product label (< 0 unresolved)
-    int32_t* H;              // [slot][nStride][LB] hop label (-1 unresolved)
-    int32_t* P;              // [slot][nStride][LB] chosen IN-arc (| TIE_AMB), -1 none
+    BLabel* L;               // [slot][nStride][LB] labels + chosen in-arc
     int32_t* queue;          // [slot][nStride] phase candidate list
     int32_t* next;           // next batch to take (device counter, zeroed per launch)
     int64_t nStride;         // >= n, multiple of 64

@@ -856,18 +856,15 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     }
     sh->batchRound = (int32_t)roundB;
     sh->batchSlots = (int32_t)slots;
-    void *D, *R, *H, *P, *q, *rows, *amb, *fl;
-    if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8)) || (rc = dev_alloc(sh, &R, slots * NS * LB * 8)) ||
-        (rc = dev_alloc(sh, &H, slots * NS * LB * 4)) || (rc = dev_alloc(sh, &P, slots * NS * LB * 4)) ||
+    void *D, *L, *q, *rows, *amb, *fl;
+    if ((rc = dev_alloc(sh, &D, roundB * NS * LB * 8)) || (rc = dev_alloc(sh, &L, slots * NS * LB * 16)) ||
         (rc = dev_alloc(sh, &q, slots * NS * 4 + 64)) ||
         (rc = dev_alloc(sh, &rows, ((size_t)sh->rowsCap + 64) * 4)) ||
         (rc = dev_alloc(sh, &amb, (size_t)sh->rowsCap + 64)) || (rc = dev_alloc(sh, &fl, roundB * 4 + 64)))
         return rc;
     sh->bsc.flags = (int32_t*)fl;
     sh->bsc.D = (unsigned long long*)D;
-    sh->bsc.R = (double*)R;
-    sh->bsc.H = (int32_t*)H;
-    sh->bsc.P = (int32_t*)P;
+    sh->bsc.L = (BLabel*)L;
     sh->bsc.queue = (int32_t*)q;
     sh->bsc.next = (int32_t*)q + slots * NS;
     sh->bsc.nStride = (int64_t)NS;
