@@ -48,9 +48,18 @@ constexpr int BKP = 3;       // in-arcs per vertex per load batch (predecessor p
 // WPE = waves per SIMD the kernel is compiled for: 4 (128 VGPRs, one
 // 1024-thread workgroup per CU, two vertices interleaved per group) or 8
 // (64 VGPRs, two workgroups per CU, one vertex per group)
+// (experiment knobs for same-box A/B builds, tools/build_variant.sh -D...)
+#ifndef SHDPE_W4_BV
+#define SHDPE_W4_BV 2
+#endif
+#ifndef SHDPE_W4_BK
+#define SHDPE_W4_BK 3
+#endif
 template <int WPE> struct BCfg {
-    static constexpr int BV = WPE >= 6 ? 1 : 2;      // vertices interleaved per group
+    static constexpr int BV = WPE >= 6 ? 1 : SHDPE_W4_BV;   // vertices interleaved per group
     static constexpr int SMAX = WPE >= 6 ? 8 : 16;   // label-walk stack: (entry, arc) pairs per thread
+    static constexpr int BKR = WPE >= 6 ? BK : SHDPE_W4_BK;   // dist gathers per vertex in flight
+    static constexpr int BKQ = WPE >= 6 ? BKP : SHDPE_W4_BK;
 };
 constexpr int WALK_BUDGET = 2048;   // walk steps per target before the deep-tree sweeps
 // Lane policy of the relaxation: a vertex with ANY dirty lane below the
@@ -251,7 +260,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     // pipelined three takes deep with lane-distributed arc records (round 5:
     // C4 N=1 106 -> 98.4 ms, N=8 shards 19.4 -> 18.9 ms same box, r05f;
     // profiles/r05_ab_notes.txt); BKR / BKQ = dist gathers per vertex in flight
-    constexpr int BKR = BK, BKQ = BKP;
+    constexpr int BKR = BCfg<WPE>::BKR, BKQ = BCfg<WPE>::BKQ;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int tieSlot[LB];
     __shared__ int laneRow[LB];           // table row of each lane (-1: pad)
