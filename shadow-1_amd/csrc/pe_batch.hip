@@ -45,6 +45,7 @@ namespace shdpe {
 constexpr int BT_THREADS = 1024;
 constexpr int BK = 3;        // arcs per vertex per load batch (relaxation)
 constexpr int BKP = 3;       // in-arcs per vertex per load batch (predecessor pass)
+constexpr int PRED_HEAVY = 64;   // predecessor pass: in-degree of a wave-scanned entry
 // WPE = waves per SIMD the kernel is compiled for: 4 (128 VGPRs, one
 // 1024-thread workgroup per CU, two vertices interleaved per group) or 8
 // (64 VGPRs, two workgroups per CU, one vertex per group)
@@ -712,6 +713,14 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             // listed in Q, targets first, then round by round the tree
             // parents of the last round's entries in every lane
             const Bits<GB> clm = par ? any0 : any1;
+            // entries of in-degree >= PRED_HEAVY are set aside per round and
+            // scanned by a whole wave each (its groups split the in-arcs and
+            // combine by cross-group shuffles): one group on a hub's ~1000
+            // in-arcs would set the round's length.  List in the LDS beyond
+            // the bitmaps (free until the label walks), capped by that room.
+            int* const heavyList = reinterpret_cast<int*>(smem + BCTRL_BYTES + (GB ? 0 : 8 * nwp));
+            const int stackB = NT * SMAX * 8, bitsB = GB ? 0 : 8 * nwp;
+            const int hcap = min(4096, max(0, stackB - bitsB) / 4);
             int lo = 0, hi = n;
             if (!fullPred) {
                 for (int j = tid; j < g.T; j += NT) {
@@ -782,7 +791,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 for (int v = 0; v < BV; ++v) ld_head(v2[v], d2[v], a02[v], a12[v]);
 #pragma unroll
                 for (int v = 0; v < BV; ++v) v3[v] = item(v0 + 3 * S + v);
-                bool root[BV];
+                bool root[BV], hvy[BV];
                 unsigned long long best[BV], mn[BV];
                 int cnt[BV], ba[BV], bu[BV], deg[BV], maxd = 0;
 #pragma unroll
@@ -794,6 +803,17 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     ba[v] = -1;
                     bu[v] = -1;
                     deg[v] = vC[v] >= 0 ? a1C[v] - a0C[v] : 0;   // group-uniform
+                    hvy[v] = false;
+                    if (deg[v] >= PRED_HEAVY) {                   // -> the round's wave pass
+                        int slot = 0;
+                        if (l == 0) slot = atomicAdd(&ctl->htail, 1);
+                        slot = __shfl(slot, gbase, 64);
+                        if (slot < hcap) {
+                            if (l == 0) heavyList[slot] = vC[v];
+                            hvy[v] = true;
+                            deg[v] = 0;
+                        }
+                    }
                     maxd = max(maxd, deg[v]);
                 }
                 for (int c0 = 0; c0 < maxd; c0 += LB) {
@@ -851,7 +871,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 #pragma unroll
                 for (int v = 0; v < BV; ++v) {
                     const int vv = vC[v];
-                    if (vv < 0) continue;
+                    if (vv < 0 || hvy[v]) continue;
                     const size_t e = (size_t)vv * LB + l;
                     const bool bad = !root[v] && mn[v] < dC[v];
                     if (bad) {
@@ -872,7 +892,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 if (!fullPred) {
 #pragma unroll
                     for (int v = 0; v < BV; ++v) {
-                        const int p = vC[v] >= 0 ? bu[v] : -1;
+                        const int p = vC[v] >= 0 && !hvy[v] ? bu[v] : -1;
                         wave_append(Q, &ctl->qtail, p >= 0 && !clm.test_set(p), p);
                     }
                 }
@@ -883,6 +903,115 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     v1[v] = v2[v]; d1[v] = d2[v]; a01[v] = a02[v]; a11[v] = a12[v];
                     v2[v] = v3[v];
                 }
+            }
+            {
+                // the round's heavy entries, one wave each
+                fence_wg();
+                __syncthreads();
+                const int nh = min(uni(ctl->htail), hcap);
+                constexpr int GPW = 64 / LB;
+                const int wv = tid >> 6, NW = NT >> 6, gw = (tid & 63) / LB;
+                for (int h = wv; h < nh; h += NW) {
+                    const int vv = __builtin_amdgcn_readfirstlane(ld_wg(&heavyList[h]));
+                    const unsigned long long dv = dec(ld_wg(&D[(size_t)vv * LB + l]));
+                    const int a0 = undirected ? g.rowPtr[vv] : g.inPtr[vv];
+                    const int a1 = undirected ? g.rowPtr[vv + 1] : g.inPtr[vv + 1];
+                    const int deg = a1 - a0;
+                    const bool root = vv == src || src < 0;
+                    unsigned long long best = INF_BITS, mn = INF_BITS;
+                    int cnt = 0, ba = -1, bu = -1;
+                    for (int c0 = gw * LB; c0 < deg; c0 += GPW * LB) {
+                        int mc;
+                        double ml;
+                        {
+                            const int a = a0 + c0 + l;
+                            const bool ok = a < a1;
+                            const int ac = ok ? a : 0;
+                            if (undirected) {
+                                const Arc A = g.arcs[ac];
+                                mc = A.col;
+                                ml = A.lat;
+                            } else {
+                                mc = g.inCol[ac];
+                                ml = g.inLat[ac];
+                            }
+                            mc = ok ? mc : -1;
+                        }
+                        const int cn = min(LB, deg - c0);
+                        for (int t = 0; t < cn; t += BKQ) {
+                            int cu[BKQ];
+                            double lw[BKQ];
+                            unsigned long long du[BKQ];
+#pragma unroll
+                            for (int k = 0; k < BKQ; ++k) {
+                                const int srcL = gbase + min(t + k, LB - 1);
+                                const int c = __shfl(mc, srcL, 64);
+                                lw[k] = __shfl(ml, srcL, 64);
+                                cu[k] = t + k < cn ? c : -1;
+                            }
+#pragma unroll
+                            for (int k = 0; k < BKQ; ++k) {
+                                const unsigned long long t2 =
+                                    dec(ld_wg(&D[(size_t)(cu[k] >= 0 ? cu[k] : 0) * LB + l]));
+                                du[k] = cu[k] >= 0 ? t2 : INF_BITS;
+                            }
+#pragma unroll
+                            for (int k = 0; k < BKQ; ++k) {
+                                if (cu[k] < 0 || root) continue;
+                                const double cand = b2d(du[k]) + lw[k];
+                                const unsigned long long cb = d2b(cand);
+                                mn = cb < mn ? cb : mn;
+                                if (dv != INF_BITS && du[k] <= dv && cand == b2d(dv)) {
+                                    if (du[k] < best) {
+                                        best = du[k];
+                                        cnt = 1;
+                                        ba = a0 + c0 + t + k;
+                                        bu = cu[k];
+                                    } else if (du[k] == best) {
+                                        ++cnt;
+                                    }
+                                }
+                            }
+                        }
+                    }
+                    // combine the groups' scans (lane l of every group holds
+                    // source l): counts of equal minima add up, so an entry is
+                    // ambiguous exactly as after one sequential scan
+                    for (int o = LB; o < 64; o <<= 1) {
+                        const unsigned long long ob = __shfl_xor(best, o, 64), om = __shfl_xor(mn, o, 64);
+                        const int oc = __shfl_xor(cnt, o, 64), oa = __shfl_xor(ba, o, 64), ou = __shfl_xor(bu, o, 64);
+                        mn = om < mn ? om : mn;
+                        if (ob < best) {
+                            best = ob; cnt = oc; ba = oa; bu = ou;
+                        } else if (ob == best && ob != INF_BITS) {
+                            cnt += oc;
+                            if (oa >= 0 && (ba < 0 || oa < ba)) { ba = oa; bu = ou; }
+                        }
+                    }
+                    const size_t e = (size_t)vv * LB + l;
+                    const bool bad = !root && mn < dv;
+                    if (bad && gw == 0) {
+                        D[e] = enc_dirty(mn);
+                        viol = 1;
+                    }
+                    const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
+                    if (bm && l == 0 && gw == 0) anyC.set(vv);
+                    const bool tree = !root && dv != INF_BITS && ba >= 0;
+                    const bool ea = !root && dv != INF_BITS && (cnt != 1 || best == dv);
+                    const int hx = tree ? ba : -1;
+                    if (gw == 0) {
+                        const bool isSrc = vv == src;
+                        lbl_st(&LBL[e], isSrc ? 1.0 : -1.0, isSrc ? 0 : -1,
+                               ea ? (TIE_AMB | (hx > 0 ? hx : 0)) : hx);
+                    }
+                    if (!fullPred) {
+                        const int p = tree ? bu : -1;
+                        wave_append(Q, &ctl->qtail, gw == 0 && p >= 0 && !clm.test_set(p), p);
+                    }
+                }
+                fence_wg();
+                __syncthreads();
+                if (tid == 0) ctl->htail = 0;   // (every thread read it before the barrier)
             }
             if (fullPred) break;
             fence_wg();
