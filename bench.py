@@ -442,6 +442,8 @@ def main():
     if rank == 0 and world == 1 and args.host_fill:
         out["host_fill"] = host_fill(eng, top)
     eng.close()
+    if rank == 0 and world == 1 and args.host_fill:
+        host_fill_image(out["host_fill"], top, att, dbg)
     if rank == 0 and world == 1 and args.secondary:
         out["secondary"] = [secondary(wl, args.steps, dbg) for wl in args.secondary.split(",") if wl]
     if rank == 0 and world == 1 and args.tie_stress:
@@ -494,13 +496,16 @@ def secondary(workload, steps, dbg):
 
 def host_fill(eng, top, block=1024, threads=0):
     """End-to-end path-cache fill as the drop-in does it (topology.c:1805-1864
-    for every row), outside `value`, two ways after one more compute:
-    (1) shd_pe_fill_rowstore: the device packs the row store's triangular
-        image (17 B per unordered pair), one DMA into page-locked memory the
-        store adopts -- the headline `end_to_end_over_compute`;
-    (2) rows DMA'd in blocks into page-locked buffers (shd_pe_get_rows) and
-        stored with shd_rowstore_store_rows, the next block's copy overlapping
-        the current block's store (`rows_path`)."""
+    for every row), outside `value`, two ways:
+    (1) shd_pe_fill_rowstore on a fresh engine (host_fill_image below): the
+        call computes the table while a host thread prepares the page-locked
+        image, then the device packs the row store's triangular image (17 B
+        per unordered pair) and one DMA lands it in the memory the store
+        adopts -- the headline `end_to_end_over_compute`;
+    (2) here, after one more compute_all: rows DMA'd in blocks into
+        page-locked buffers (shd_pe_get_rows) and stored with
+        shd_rowstore_store_rows, the next block's copy overlapping the
+        current block's store (`rows_path`)."""
     import threading
     from shdpe.engine import RowStore
     T = eng.T
@@ -510,14 +515,6 @@ def host_fill(eng, top, block=1024, threads=0):
     eng.compute_all()
     eng.synchronize()
     t_gpu = time.perf_counter() - t0
-    img = RowStore(top.n, eng.attached)
-    i0 = time.perf_counter()
-    ok, ms = eng.fill_rowstore(img)
-    t_img = time.perf_counter() - i0
-    image = {"ms_fill": t_img * 1e3, "ms_alloc": ms["alloc"], "ms_pack": ms["pack"], "ms_dma": ms["dma"],
-             "image_GB": img.memory_bytes() / 1e9, "entries_stored": int(img.size()),
-             "rows_all_success": int(ok.sum())}
-    img.close()
     store = RowStore(top.n, eng.attached)
     fields = ("lat", "rel", "flags")
     bufs = [eng.pinned_rows(min(block, count), fields) for _ in range(2)]
@@ -553,17 +550,39 @@ def host_fill(eng, top, block=1024, threads=0):
                  "how": "shd_pe_get_rows into shd_pe_host_alloc buffers (lat, rel, flags) + "
                         "shd_rowstore_store_rows (threads by slot rows), copy of block b+1 "
                         "overlapping the store of block b"}
-    assert rows_path["entries_stored"] == image["entries_stored"], (rows_path, image)
-    out = {"rows": int(count), "ms_compute": t_gpu * 1e3, **image,
-           "host_fill_rows_per_s": count / (t_gpu + t_img),
-           "end_to_end_over_compute": (t_gpu + t_img) / t_gpu,
-           "end_to_end_over_compute_excl_alloc": (t_gpu + t_img - ms["alloc"] * 1e-3) / t_gpu,
-           "how": "compute_all + shd_pe_fill_rowstore (device-packed triangular cache image, one DMA "
-                  "into page-locked memory the row store adopts; allocation included)",
-           "rows_path": rows_path}
+    out = {"rows": int(count), "ms_compute": t_gpu * 1e3, "rows_path": rows_path}
     store.close()
     del bufs
     return out
+
+
+def host_fill_image(out, top, att, dbg):
+    """The drop-in's one call on a freshly built engine (graph upload
+    untimed; no variant pick -- the drop-in computes once, so its first
+    compute runs the default variant and allocates its scratch inside the
+    timed call): shd_pe_fill_rowstore computes every row, with the host image
+    prepared on a host thread meanwhile, packs and DMAs it.  The ratio is that
+    call's wall time over the tuned compute_all's (`ms_compute`, same box)."""
+    from shdpe.engine import Engine, RowStore
+    eng = Engine(top, att, debug_flags=dbg)
+    eng.synchronize()
+    img = RowStore(top.n, eng.attached)
+    i0 = time.perf_counter()
+    ok, ms = eng.fill_rowstore(img)
+    t_img = time.perf_counter() - i0
+    t_gpu = out["ms_compute"] * 1e-3
+    out.update({"ms_fill": t_img * 1e3, "ms_compute_and_image_prep": ms["alloc"], "ms_pack": ms["pack"],
+                "ms_dma": ms["dma"], "image_GB": img.memory_bytes() / 1e9,
+                "entries_stored": int(img.size()), "rows_all_success": int(ok.sum()),
+                "host_fill_rows_per_s": out["rows"] / t_img,
+                "end_to_end_over_compute": t_img / t_gpu,
+                "how": "fresh engine, one shd_pe_fill_rowstore call: compute_all on the device while a "
+                       "host thread maps, first-touches (16 threads, huge pages) and registers the "
+                       "image; device pack of the triangular cache image; one DMA into it; the row "
+                       "store adopts it"})
+    assert out["rows_path"]["entries_stored"] == out["entries_stored"], out
+    img.close()
+    eng.close()
 
 
 def tie_stress(workload, steps, dbg):

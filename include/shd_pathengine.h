@@ -278,14 +278,17 @@ int shd_pe_put_rows(ShdPe* pe, int32_t start, int32_t count, const double* lat, 
 int shd_pe_row_checksums(ShdPe* pe, int32_t start, int32_t count, uint64_t* out);
 
 /* The whole-table path-cache fill in one pass: rows 0..T-1 (computed first
- * if needed; a sharded engine must be gathered) into an EMPTY row store, with
+ * if needed -- then the host image is prepared on a host thread while the
+ * device computes, so the drop-in's cheapest call is this one alone; a
+ * sharded engine must be gathered) into an EMPTY row store, with
  * exactly the result of shd_rowstore_store_rows over every row in position
  * order (isComplete from the graph, no prefersDirectPaths adjacency --
  * topology.c:1805-1864 per row).  The device packs the store's triangular
  * row image (shd_rowstore_image_layout: 17 B per unordered pair instead of
  * 34 B of two rows) and one DMA lands it in page-locked memory the store
  * adopts.  rowResult (optional, T entries): each row's store_row result.
- * msOut (optional, 3 entries): ms of allocation, device pack, DMA. */
+ * msOut (optional, 3 entries): ms of compute (if any) overlapped with the
+ * host image preparation, device pack, DMA. */
 struct ShdRowStore;
 int shd_pe_fill_rowstore(ShdPe* pe, struct ShdRowStore* st, int32_t* rowResult, double* msOut);
 

@@ -18,6 +18,7 @@
 // under graphLock (topology.c:1747-1781).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -828,7 +829,7 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const size_t NS = ((size_t)pe->hg.n + 63) & ~(size_t)63;
     const size_t LB = (size_t)sh->bcfg.lb;
     const size_t bitBytes = sh->bcfg.gbits ? (size_t)batch_bits_words(pe->hg.n) * 4 : 0;
-    const size_t perSlot = NS * LB * (8 + 8 + 4 + 4) + NS * 4 + bitBytes;
+    const size_t perSlot = NS * LB * (8 + 16) + NS * 4 + bitBytes;   // D, L
     // scratch budget (default 64 GiB): fewer resident batches on huge graphs
     const double budget = pe->tu.batchScratchGB * (double)(1ull << 30);
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
@@ -1755,39 +1756,100 @@ extern "C" int shd_pe_row_checksums(ShdPe* pe, int32_t start, int32_t count, uin
 // position order) as one device pass: k_pack_rowstore builds the row
 // store's own image of its triangular rows (2.3 GB at C4 vs 7.8 GB of
 // rows), one DMA lands it in page-locked host memory the store adopts.
-static void host_free_cb(void*, void* p) { (void)hipHostFree(p); }
+//
+// The host image (2.3 GB at C4) is anonymous memory with transparent huge
+// pages, first-touched by 16 threads and then registered with the device
+// (page-locked): hipHostMalloc of the same size took 430 ms, most of it
+// faulting and zeroing 4-KB pages on one thread.  When the rows still have
+// to be computed, that preparation runs on a host thread while the device
+// computes them.
+struct HostImage {
+    void* p = nullptr;
+    size_t bytes = 0;
+    bool registered = false;
+    double msTouch = 0.0, msRegister = 0.0;
+};
+
+static void host_image_prepare(HostImage* im, size_t bytes) {
+    const auto t0 = std::chrono::steady_clock::now();
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (p == MAP_FAILED) return;
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+    const size_t nt = 16, chunk = ((bytes + nt - 1) / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; ++t)
+        th.emplace_back([=] {
+            unsigned char* q = static_cast<unsigned char*>(p);
+            for (size_t o = t * chunk; o < std::min(bytes, (t + 1) * chunk); o += 4096) q[o] = 0;
+        });
+    for (auto& x : th) x.join();
+    im->p = p;
+    im->bytes = bytes;
+    const auto t1 = std::chrono::steady_clock::now();
+    im->registered = hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess;
+    const auto t2 = std::chrono::steady_clock::now();
+    im->msTouch = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    im->msRegister = std::chrono::duration<double, std::milli>(t2 - t1).count();
+}
+
+static void host_image_release(HostImage* im) {
+    if (!im->p) return;
+    if (im->registered) (void)hipHostUnregister(im->p);
+    (void)munmap(im->p, im->bytes);
+    im->p = nullptr;
+}
+
+static void host_image_free_cb(void* ctx, void* p) {
+    HostImage* im = static_cast<HostImage*>(ctx);
+    (void)p;
+    host_image_release(im);
+    delete im;
+}
 
 extern "C" int shd_pe_fill_rowstore(ShdPe* pe, ShdRowStore* st, int32_t* rowResult, double* msOut) {
     if (!pe || !st) return SHD_PE_EINVAL;
     if (shd_rowstore_size(st) != 0) return SHD_PE_EINVAL;   // (adopt_image re-checks under its lock)
     const int32_t T = (int32_t)pe->attached.size();
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::vector<int64_t> off((size_t)T + 1);
+    shd_rowstore_image_layout(T, off.data());
+    const size_t bytes = (size_t)off[(size_t)T];
+    const bool pack = !pe->hg.isComplete;    // a complete graph stores no non-direct path (:1321)
+    const auto t0 = now();
+    std::unique_ptr<HostImage> him(new HostImage);
+    std::thread prep;
+    if (pack) prep = std::thread(host_image_prepare, him.get(), bytes);   // beside the compute
     int rc = ensure_rows(pe, 0, T);
-    if (rc) return rc;
+    const auto tc = now();
+    if (prep.joinable()) prep.join();
+    if (std::getenv("SHDPE_FILL_LOG"))
+        std::fprintf(stderr, "[shdpe] fill_rowstore: compute %.1f ms, image %.2f GB touch %.1f ms + "
+                     "register %.1f ms (%s), join wait %.1f ms\n", ms(t0, tc), bytes / 1e9, him->msTouch,
+                     him->msRegister, him->registered ? "registered" : "NOT registered", ms(tc, now()));
+    if (rc) { host_image_release(him.get()); return rc; }
+    if (pack && !him->p) return SHD_PE_ENOMEM;
     std::lock_guard<std::mutex> lk(pe->copyMu);
     const DevTable* tab = nullptr;
     Shard* s = pe->shards[0].get();
     if (pe->gathered) tab = &s->full;
     else if (pe->G == 1) tab = &s->tab;
     else return SHD_PE_ENOTOWNED;          // rows spread over shards: gather first
-    HIPCHK(hipSetDevice(s->device));
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    std::vector<int64_t> off((size_t)T + 1);
-    shd_rowstore_image_layout(T, off.data());
-    const size_t bytes = (size_t)off[(size_t)T];
-    const auto t0 = now();
-    void *dImg = nullptr, *dOff = nullptr, *dAcc = nullptr, *dAll = nullptr, *hImg = nullptr;
-    struct Free {   // device temporaries, every exit path
+    if (hipSetDevice(s->device) != hipSuccess) { host_image_release(him.get()); return SHD_PE_EHIP; }
+    void *dImg = nullptr, *dOff = nullptr, *dAcc = nullptr, *dAll = nullptr;
+    void* const hImg = him->p;
+    struct Free {   // device temporaries (and the host image until adopted), every exit path
         void** p[4];
-        ~Free() { for (void** q : p) if (*q) (void)hipFree(*q); }
-    } fr{{&dImg, &dOff, &dAcc, &dAll}};
-    const bool pack = !pe->hg.isComplete;    // a complete graph stores no non-direct path (:1321)
-    if ((pack && (hipMalloc(&dImg, bytes) != hipSuccess || hipHostMalloc(&hImg, bytes) != hipSuccess)) ||
+        std::unique_ptr<HostImage>* h;
+        ~Free() {
+            for (void** q : p) if (*q) (void)hipFree(*q);
+            if (*h) host_image_release(h->get());
+        }
+    } fr{{&dImg, &dOff, &dAcc, &dAll}, &him};
+    if ((pack && hipMalloc(&dImg, bytes) != hipSuccess) ||
         hipMalloc(&dOff, off.size() * 8) != hipSuccess || hipMalloc(&dAcc, 16) != hipSuccess ||
-        hipMalloc(&dAll, (size_t)T * 4) != hipSuccess) {
-        if (hImg) (void)hipHostFree(hImg);
+        hipMalloc(&dAll, (size_t)T * 4) != hipSuccess)
         return SHD_PE_ENOMEM;
-    }
     const auto t1 = now();
     const unsigned long long acc0[2] = {0ull, 0x7FF0000000000000ull};
     unsigned long long acc[2] = {0ull, 0ull};
@@ -1808,15 +1870,14 @@ extern "C" int shd_pe_fill_rowstore(ShdPe* pe, ShdRowStore* st, int32_t* rowResu
         e = hipMemcpyAsync(rowResult, dAll, (size_t)T * 4, hipMemcpyDeviceToHost, s->copyStream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->copyStream);
     const auto t3 = now();
-    if (e != hipSuccess) {
-        if (hImg) (void)hipHostFree(hImg);
-        return SHD_PE_EHIP;
-    }
+    if (e != hipSuccess) return SHD_PE_EHIP;
     if (pack) {
         double mn;
         std::memcpy(&mn, &acc[1], 8);
-        rc = shd_rowstore_adopt_image(st, hImg, (int64_t)bytes, host_free_cb, nullptr, (int64_t)acc[0], mn);
-        if (rc) { (void)hipHostFree(hImg); return rc; }
+        rc = shd_rowstore_adopt_image(st, hImg, (int64_t)bytes, host_image_free_cb, him.get(),
+                                      (int64_t)acc[0], mn);
+        if (rc) return rc;
+        him.release();   // the store owns it now
     }
     if (msOut) { msOut[0] = ms(t0, t1); msOut[1] = ms(t1, t2); msOut[2] = ms(t2, t3); }
     return SHD_PE_OK;

@@ -1137,6 +1137,14 @@ struct WHeap {
     // round, so a sift-down touches the global tail once.
     __device__ __forceinline__ bool sink_round(int& head, int& hl, double k, int id, int size,
                                                int ldsLevel, int lane) const {
+        // every operand but the lane's own node is wave-uniform: say so, so
+        // the descent bookkeeping is scalar code, not exec-masked VALU loops
+        head = __builtin_amdgcn_readfirstlane(head);
+        hl = __builtin_amdgcn_readfirstlane(hl);
+        size = __builtin_amdgcn_readfirstlane(size);
+        ldsLevel = __builtin_amdgcn_readfirstlane(ldsLevel);
+        k = readlane_f64(k, 0);
+        id = __builtin_amdgcn_readfirstlane(id);
         const int bottom = 31 - __builtin_clz(size);       // deepest heap level
         int dd = bottom - hl < 5 ? bottom - hl : 5;
         if (dd <= 0) {
@@ -1197,6 +1205,9 @@ struct WHeap {
     }
     // igraph_i_2wheap_shift_up of (k, id) from the hole at `elem`
     __device__ __forceinline__ void shift_up(int elem, double k, int id, int lane) const {
+        elem = __builtin_amdgcn_readfirstlane(elem);
+        k = readlane_f64(k, 0);
+        id = __builtin_amdgcn_readfirstlane(id);
         const int a = lane < 31 ? ((elem + 1) >> (lane + 1)) - 1 : -1;
         const bool valid = a >= 0;
         const bool lds = elem < hc;                      // every ancestor and the hole
@@ -1239,6 +1250,9 @@ __device__ __forceinline__ uint32_t warm_cache(const void* p, size_t bytes, int 
     return acc;
 }
 
+// XD: per-pop segment counters (SHD_PE_DEBUG_COUNTERS; a separate
+// instantiation so the product build carries none of their registers)
+template <bool XD>
 __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable tab0,
                                                            DevScratch sc0,
                                                            const int32_t* __restrict__ rows,
@@ -1269,10 +1283,10 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
     }
 
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
-        const int r = rows[b];
-        const int s = g.attached[r];
-        const int tslot = slots ? slots[b] : -1;
-        const double thr = tslot >= 0 ? tie.thr[tslot] : 0.0;
+        const int r = __builtin_amdgcn_readfirstlane(rows[b]);
+        const int s = __builtin_amdgcn_readfirstlane(g.attached[r]);
+        const int tslot = __builtin_amdgcn_readfirstlane(slots ? slots[b] : -1);
+        const double thr = readlane_f64(tslot >= 0 ? tie.thr[tslot] : 0.0, 0);
         if (tslot < 0 || thr >= 0.0)
             for (int v = lane; v < n; v += EX_THREADS) h.I2[v] = 0;
         __syncthreads();
@@ -1289,9 +1303,9 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
         // SHD_PE_DEBUG_COUNTERS: cycles per pop segment (top+range, sink,
         // arcs+pre-check, pushes), pops, pushes + modifies, heap size at exit
         long long xc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        long long xt = xdbg ? (long long)clock64() : 0;
+        long long xt = XD ? (long long)clock64() : 0;
         auto xtick = [&](int k) {
-            if (xdbg) { const long long t = (long long)clock64(); xc[k] += t - xt; xt = t; }
+            if constexpr (XD) { const long long t = (long long)clock64(); xc[k] += t - xt; xt = t; }
         };
         // early-stop rows need only the parents (k_tie_write derives hops and
         // reliability); a relevance scan may have cleared the row (thr < 0)
@@ -1313,7 +1327,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
             double km = 0.0;
             int im = 0;
             if (size > 0) h.get(size, km, im);       // uniform position: last element
-            if (xdbg) { asm volatile("" :: "v"(a0), "v"(a1), "v"(att)); xtick(0); xc[5]++; }
+            if constexpr (XD) { asm volatile("" :: "v"(a0), "v"(a1), "v"(att)); xtick(0); xc[5]++; }
             if (lane == 0) h.I2[u] = 1;
             int head = 0, hl = 0;
             bool placed = size == 0;
@@ -1356,7 +1370,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                 }
                 unsigned long long mask = __ballot(need != 0);
                 xtick(2);
-                if (xdbg) xc[6] += __builtin_popcountll(mask);
+                if constexpr (XD) xc[6] += __builtin_popcountll(mask);
                 bool moved = !posFresh;    // positions read in the pre-check stale?
                 while (mask) {
                     const int k = __builtin_ctzll(mask);
@@ -1376,7 +1390,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                 xtick(3);
             }
         }
-        if (xdbg && lane == 0) {
+        if (XD && lane == 0) {
             xc[7] = size;
             for (int k = 0; k < 8; ++k) xdbg[(size_t)b * 8 + k] = xc[k];
         }
@@ -1841,10 +1855,17 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
         return;
     }
     const int bytes = (int)(((size_t)12 * hc + 15) & ~(size_t)15);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    hipLaunchKernelGGL(k_exact_rows, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc, dRows,
-                       nRows, hc, dSlots, tie, dXdbg);
+    if (dXdbg) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipLaunchKernelGGL(k_exact_rows<true>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc,
+                           dRows, nRows, hc, dSlots, tie, dXdbg);
+        return;
+    }
+    hipLaunchKernelGGL(k_exact_rows<false>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc,
+                       dRows, nRows, hc, dSlots, tie, dXdbg);
 }
 
 void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,

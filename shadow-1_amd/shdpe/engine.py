@@ -494,9 +494,10 @@ class Engine:
         return out
 
     def fill_rowstore(self, store) -> tuple:
-        """shd_pe_fill_rowstore: the whole table into an empty RowStore in one
+        """shd_pe_fill_rowstore: the whole table (computed first if needed,
+        the host image prepared meanwhile) into an empty RowStore in one
         device pack + DMA; returns (per-row store_row results, ms of
-        allocation / pack / DMA)."""
+        compute-and-image-preparation ("alloc") / pack / DMA)."""
         res = np.empty(self.T, np.int32)
         ms = np.zeros(3)
         self._chk(self._lib.shd_pe_fill_rowstore(self.h, store.h, _p(res), _p(ms)), "shd_pe_fill_rowstore")

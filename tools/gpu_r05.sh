@@ -11,6 +11,9 @@
 #   default   the driver's command (python bench.py, all legs)
 #   trace     rocprofv3 --kernel-trace --stats of quick bench lines for $WLS
 #   pmc       FETCH_SIZE / WRITE_SIZE / TCC hit+miss passes -> traffic_<wl>.json
+#   hostfill  bench's host_fill block alone (C4)
+#   exactdbg  k_exact_rows per-pop cycle counters on c4q (SHDPE_DEBUG)
+#   exactpmc  k_exact_rows SQ instruction counters on c4q
 # usage: STAGES="tests bench" tools/gpu_r05.sh TAG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd $R
@@ -84,5 +87,17 @@ for st in ${STAGES:-tests bench}; do
       done
       python3 tools/traffic_json.py $OUT $wl $TAG $OUT/traffic_$wl.json $OUT/${TAG}_${wl}_pmc || exit 1
     done ;;
+  hostfill)
+    # the host_fill block alone (C4: rows path + fresh-engine fill_rowstore)
+    timeout -k 10 400 python3 -u bench.py --workload c4 --steps 3 --warmup 1 --no-cpu --tie-stress= --secondary= --d2h-rows 0 --no-stream > $OUT/hostfill.json 2> $OUT/hostfill.err || { tail -20 $OUT/hostfill.err; exit 1; }
+    python3 -c "import json; h=json.load(open('$OUT/hostfill.json'))['host_fill']; print({k: (round(v, 3) if isinstance(v, float) else v) for k, v in h.items() if k not in ('how', 'rows_path')}); print('rows_path', {k: (round(v, 3) if isinstance(v, float) else v) for k, v in h['rows_path'].items() if k != 'how'})" ;;
+  exactdbg)
+    # k_exact_rows per-pop segment counters (SHDPE_DEBUG) on the c4q tie rows
+    SHDPE_DEBUG=1 timeout -k 10 300 python3 -u bench.py --workload c4q --steps 1 --warmup 0 $QUICK > $OUT/exactdbg.json 2> $OUT/exactdbg.err || { tail -20 $OUT/exactdbg.err; exit 1; }
+    grep "exact row" $OUT/exactdbg.err | sort -t= -k2 -n -r | head -20 || true ;;
+  exactpmc)
+    # instruction mix of the exact kernel (SQ counters, one pass)
+    (cd /tmp && TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY --output-format csv -d $R/$OUT/exactpmc -o pmc -- python3 $R/bench.py --workload c4q --steps 1 --warmup 0 $QUICK > $R/$OUT/exactpmc.log 2>&1) || { echo "exact pmc failed"; tail -5 $OUT/exactpmc.log; exit 1; }
+    find $OUT/exactpmc -name "*counter_collection.csv" | head -1 | xargs grep -h "k_exact_rows" | head -20 || true ;;
   esac
 done
