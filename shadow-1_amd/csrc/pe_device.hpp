@@ -189,6 +189,7 @@ void launch_sparse_rows(const DevGraph& g, const DevTable& tab, const DevScratch
 // parents in tie.P for launch_tie_write
 // hc: heap positions held in LDS (k_exact_rows, n > exact_soa_max_n());
 // forceGlobalHeap: k_exact_rows even when the SoA all-LDS kernel would fit
+int exact_bits_bytes(int n);
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
                        bool forceGlobalHeap, const int32_t* dSlots, const TieBuf& tie,

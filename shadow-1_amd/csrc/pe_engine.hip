@@ -275,8 +275,12 @@ static int configure(ShdPe* pe, Shard* sh) {
     // tail in the global slot.
     const bool soa = n <= exact_soa_max_n() && tu.exactHc <= 0;
     const long perWG = soa ? 16L * n + 16 : std::min<long>(LDS, 12L * n + 16);
-    // (512 B of the LDS stay free for the kernels' static shared variables)
-    sh->exactHc = (int)std::max<long>(1, std::min<long>(n, (std::min<long>(LDS - 512, perWG) - 16) / 12));
+    // (512 B of the LDS stay free for the kernels' static shared variables;
+    // k_exact_rows' preferred-child bits take their share when they fit in
+    // half of it -- n <= ~650k)
+    const long bitsB = !soa && exact_bits_bytes(n) <= LDS / 2 ? exact_bits_bytes(n) : 0;
+    sh->exactHc = (int)std::max<long>(
+        1, std::min<long>(n, (std::min<long>(LDS - 512 - bitsB, perWG) - 16) / 12));
     if (tu.exactHc > 0) sh->exactHc = std::min(sh->exactHc, tu.exactHc);   // tests: global heap tail
     const int exPerCU = (int)std::max<long>(1, std::min<long>(8, LDS / perWG));
     sh->exactGrid = sh->numCUs * (tu.exactPerCU > 0 ? tu.exactPerCU : exPerCU);
@@ -314,10 +318,13 @@ static int configure(ShdPe* pe, Shard* sh) {
     };
     // Two kernel variants: 8 waves per SIMD (two 1024-thread workgroups per
     // CU, one vertex per group) and 4 (one workgroup per CU, two vertices
-    // per group).  Which is faster differs from box to box of the same SKU
-    // (C4 same-box pairs: 172 vs 185 ms on some, 182 vs 142 ms on others;
-    // profiles/r03_ab_notes.txt), so the engine starts with 8 and
-    // shd_pe_tune times both; SHDPE_BATCH_WPE forces one.
+    // per group).  Which is faster differed from box to box of the same SKU
+    // in rounds 3-4 (C4 same-box pairs: 172 vs 185 ms on some, 182 vs 142 ms
+    // on others; profiles/r03_ab_notes.txt), so shd_pe_tune times them all;
+    // SHDPE_BATCH_WPE forces one.  Since the round-5 loops the tune has
+    // picked the 4-wave relax on every box (and the 6-wave post kernel for
+    // batches of 16, the 4-wave one for 8), so an untuned engine -- the
+    // drop-in computes once -- starts there.
     auto make = [&](int wpe) {
         BatchLaunch c = b;
         c.wpe = wpe;
@@ -335,7 +342,7 @@ static int configure(ShdPe* pe, Shard* sh) {
     const bool ok8 = v8.second >= 1, ok4 = v4.second >= 1, ok6 = v6.second >= 2 && b.threads == 1024;
     if (pe->batched && !ok8 && !ok4) return SHD_PE_ETOOBIG;
     if (!pe->batched && layout == 0 && need0 > LDS) return SHD_PE_ETOOBIG;
-    const int first = forced == 6 && ok6 ? 6 : forced == 4 || !ok8 ? 4 : 8;
+    const int first = forced == 6 && ok6 ? 6 : forced == 8 && ok8 ? 8 : ok4 ? 4 : 8;
     v8.first.split = v4.first.split = v6.first.split = tu.batchSplit ? 1 : 0;
     b = first == 8 ? v8.first : first == 6 ? v6.first : v4.first;
     sh->bcfgAlt = sh->bcfgAlt2 = BatchLaunch{};
@@ -345,11 +352,13 @@ static int configure(ShdPe* pe, Shard* sh) {
     if (!forced && ok6 && tu.batchSplit) sh->bcfgAlt2 = v6.first;
     (void)need0;
     sh->bcfg = b;
+    sh->bcfgPost = BatchLaunch{};
+    if (!forced && first == 4 && ok6 && b.split && b.lb >= 16) sh->bcfgPost = v6.first;
     sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
     sh->stats.batched = pe->batched ? 1 : 0;
     sh->stats.batchLanes = pe->batched ? b.lb : 0;
     sh->stats.batchWaves = pe->batched ? b.wpe : 0;
-    sh->stats.batchPostWaves = pe->batched && b.split ? b.wpe : 0;
+    sh->stats.batchPostWaves = pe->batched && b.split ? (sh->bcfgPost.grid > 0 ? sh->bcfgPost.wpe : b.wpe) : 0;
     return SHD_PE_OK;
 }
 

@@ -1097,6 +1097,7 @@ struct WHeap {
     int32_t* gidx;
     int32_t* I2;      // index2 (global, per vertex)
     int hc;
+    uint32_t* bitw;   // preferred-child bits (LDS, k_exact_rows<.., true>), see below
     __device__ __forceinline__ double* lkey() const { return reinterpret_cast<double*>(ex_smem); }
     __device__ __forceinline__ int32_t* lidx() const {
         return reinterpret_cast<int32_t*>(ex_smem + (size_t)8 * hc);
@@ -1203,6 +1204,142 @@ struct WHeap {
         hl += dd;
         return false;
     }
+    // ---- preferred-child bits (round 5) --------------------------------
+    // One bit per internal heap node, 1-based node numbering (node N =
+    // position N - 1, children 2N and 2N + 1): set iff the right child
+    // exists and its key is strictly larger, i.e. the child igraph's sink
+    // descends to from N.  Every operation that changes a key keeps the bits
+    // of the changed nodes' parents current (and a pop that removes a right
+    // child clears its parent's bit), so a sift-down finds its whole descent
+    // path from the bits alone -- six levels per LDS word round and a few
+    // scalar instructions per level -- and then loads, compares and moves
+    // only the path's nodes in ONE parallel round, instead of loading and
+    // ranking every node of each 5-level subtree (62 lanes per round, four
+    // rounds for a 16-level heap).  A node's bit is read only while it is
+    // internal and every node is re-derived when it gains a child, so the
+    // bits need no per-row initialisation.  Updates are LDS atomics (lanes
+    // of one operation may share a word).
+    __device__ __forceinline__ double get_key(int p) const {
+        double k;
+        if (p < hc) {
+            k = lkey()[p];
+            asm volatile("" : "+v"(k));
+        } else {
+            k = gkey[p - hc];
+            asm volatile("" : "+v"(k));
+        }
+        return k;
+    }
+    __device__ __forceinline__ void bit_put(int node, bool v) const {
+        const uint32_t m = 1u << (node & 31);
+        if (v) atomicOr(&bitw[node >> 5], m);
+        else atomicAnd(&bitw[node >> 5], ~m);
+    }
+    // after a pop shrank the heap to `size`: the removed node size + 1, when
+    // it was a right child, leaves its parent with the left child only
+    __device__ __forceinline__ void bits_removed(int size, int lane) const {
+        const int r = size + 1;
+        if (lane == 0 && r >= 3 && (r & 1)) bit_put(r >> 1, false);
+    }
+    // sift-down phase 1: the descent path below the root (nodes of depth
+    // 1..K in lanes 0..K-1 of pnode); returns K
+    __device__ __forceinline__ int sink_path(int size, int lane, int& pnode) const {
+        size = __builtin_amdgcn_readfirstlane(size);
+        int cur = 1, K = 0;
+        pnode = 1;
+        while (2 * cur <= size) {
+            // lane d < 6: the bit word of the level d below cur (2^d <= 32
+            // consecutive, aligned node numbers: one word)
+            const int base = lane < 6 ? cur << lane : 0;
+            uint32_t wv = 0u;
+            if (lane < 6 && base <= (size >> 1)) wv = bitw[base >> 5];
+            int d = 0;
+            for (; d < 6 && 2 * cur <= size; ++d) {
+                const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)wv, d);
+                cur = 2 * cur + (int)((w >> (cur & 31)) & 1u);
+                pnode = lane == K ? cur : pnode;
+                ++K;
+            }
+        }
+        return K;
+    }
+    // sift-down phase 2: (k, id) passes the path prefix it is strictly
+    // smaller than (igraph_i_2wheap_sink); those nodes move up one level.
+    // Split in two so the caller can issue the path's loads before it waits
+    // for anything else: sink_load issues them, sink_place uses them.
+    struct PathVals {
+        double kq, ks;
+        int iq;
+    };
+    __device__ __forceinline__ PathVals sink_load(int size, int K, int pnode, int lane) const {
+        size = __builtin_amdgcn_readfirstlane(size);
+        K = __builtin_amdgcn_readfirstlane(K);
+        const bool on = lane < K;
+        const int q = on ? pnode : 1;
+        const int sb = q ^ 1;
+        PathVals pv{0.0, 0.0, -1};
+        if (on) get(q - 1, pv.kq, pv.iq);
+        if (on && sb <= size) pv.ks = get_key(sb - 1);
+        return pv;
+    }
+    __device__ __forceinline__ void sink_place(double k, int id, int size, int K, int pnode,
+                                               const PathVals& pv, int lane) const {
+        k = readlane_f64(k, 0);
+        id = __builtin_amdgcn_readfirstlane(id);
+        size = __builtin_amdgcn_readfirstlane(size);
+        K = __builtin_amdgcn_readfirstlane(K);
+        const bool on = lane < K;
+        const int q = on ? pnode : 1;
+        const int sb = q ^ 1;
+        const bool sibOk = on && sb <= size;
+        const double kq = pv.kq, ks = pv.ks;
+        const int iq = pv.iq;
+        const unsigned long long mm = __ballot(on && k < kq);   // a prefix of the path
+        const int m = __builtin_popcountll(mm);
+        if (lane < m) put((q >> 1) - 1, kq, iq);
+        const int fin = m == 0 ? 1 : __builtin_amdgcn_readlane(pnode, m - 1);
+        if (lane == 0) put(fin - 1, k, id);
+        // node q_(t+1) (lane t < m) now holds lane t+1's key, or k
+        const double kn = __shfl_down(kq, 1, 64);
+        const double nk = lane == m - 1 ? k : kn;
+        if (lane < m) bit_put(q >> 1, (q & 1) == 0 ? (sibOk && ks > nk) : (nk > ks));
+    }
+    // igraph_i_2wheap_shift_up with the bits kept: `size` counts (k, id)
+    __device__ __forceinline__ void shift_up_bits(int elem, double k, int id, int size, int lane) const {
+        elem = __builtin_amdgcn_readfirstlane(elem);
+        k = readlane_f64(k, 0);
+        id = __builtin_amdgcn_readfirstlane(id);
+        size = __builtin_amdgcn_readfirstlane(size);
+        const int e1 = elem + 1;
+        const int x = lane < 31 ? e1 >> lane : 0;          // node x_j: e1 and its ancestors
+        const int a = lane < 31 ? e1 >> (lane + 1) : 0;    // its parent (0: none)
+        const bool valid = a >= 1;
+        const int sb = x ^ 1;
+        const bool sibOk = valid && sb <= size;
+        double ka = 0.0, ks = 0.0;
+        int ia = -1;
+        if (e1 < hc) {                                     // every node involved in LDS
+            const int ac = valid ? a - 1 : 0;
+            ka = lkey()[ac];
+            ia = lidx()[ac];
+            ks = lkey()[sibOk ? sb - 1 : 0];
+        } else {
+            if (valid) get(a - 1, ka, ia);
+            if (sibOk) ks = get_key(sb - 1);
+        }
+        const unsigned long long sm = __ballot(!valid || k < ka);
+        const int c = __builtin_ctzll(sm);                 // ancestors passed (k >= theirs)
+        if (lane < c) {
+            if (e1 < hc) put_lds(x - 1, ka, ia);
+            else put(x - 1, ka, ia);
+        }
+        if (lane == 0) put((e1 >> c) - 1, k, id);
+        // x_j (j <= c) changed: to ancestor j+1's key (j < c) or to k
+        if (lane <= c && valid) {
+            const double nk = lane < c ? ka : k;
+            bit_put(a, (x & 1) == 0 ? (sibOk && ks > nk) : (nk > ks));
+        }
+    }
     // igraph_i_2wheap_shift_up of (k, id) from the hole at `elem`
     __device__ __forceinline__ void shift_up(int elem, double k, int id, int lane) const {
         elem = __builtin_amdgcn_readfirstlane(elem);
@@ -1251,8 +1388,10 @@ __device__ __forceinline__ uint32_t warm_cache(const void* p, size_t bytes, int 
 }
 
 // XD: per-pop segment counters (SHD_PE_DEBUG_COUNTERS; a separate
-// instantiation so the product build carries none of their registers)
-template <bool XD>
+// instantiation so the product build carries none of their registers).
+// BITS: sift-downs by the preferred-child bits (LDS words after the heap
+// head; the engine sizes hc for them), else by 5-level subtree rounds.
+template <bool XD, bool BITS>
 __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable tab0,
                                                            DevScratch sc0,
                                                            const int32_t* __restrict__ rows,
@@ -1270,7 +1409,8 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
     double* R = sc.rel + slot;
     int32_t* P = sc.pred + slot;
     double* tailKey = reinterpret_cast<double*>(sc.heapTail) + (size_t)blockIdx.x * 2 * sc.heapStride;
-    const WHeap h{tailKey, reinterpret_cast<int32_t*>(tailKey + sc.heapStride), sc.index2 + slot, hc};
+    const WHeap h{tailKey, reinterpret_cast<int32_t*>(tailKey + sc.heapStride), sc.index2 + slot, hc,
+                  reinterpret_cast<uint32_t*>(ex_smem + (((size_t)12 * hc + 15) & ~(size_t)15))};
     {
         const size_t m = (size_t)g.rowPtr[n];
         uint32_t acc = warm_cache(g.rowPtr, (size_t)4 * (n + 1), lane, EX_THREADS);
@@ -1329,9 +1469,13 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
             if (size > 0) h.get(size, km, im);       // uniform position: last element
             if constexpr (XD) { asm volatile("" :: "v"(a0), "v"(a1), "v"(att)); xtick(0); xc[5]++; }
             if (lane == 0) h.I2[u] = 1;
-            int head = 0, hl = 0;
+            int head = 0, hl = 0, pK = 0, pnode = 0;
             bool placed = size == 0;
-            if (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+            if constexpr (BITS) {
+                h.bits_removed(size, lane);
+            } else {
+                if (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+            }
             if (att) --toReach;
             // arcs in chunks of 64; the first chunk's loads and pre-check
             // overlap the remaining sink rounds (the pre-check reads only
@@ -1347,7 +1491,15 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                     w = g.lat[a];
                     ia = g.outToIn[a];
                 }
-                if (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+                WHeap::PathVals pv{0.0, 0.0, -1};
+                if constexpr (BITS) {
+                    if (!placed) {
+                        pK = h.sink_path(size, lane, pnode);   // LDS words only
+                        pv = h.sink_load(size, pK, pnode, lane);   // in flight under the arc loads' wait
+                    }
+                } else {
+                    if (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+                }
                 // read before the sift-down finished: categories and distances
                 // hold, heap positions may not
                 const bool posFresh = placed;
@@ -1357,7 +1509,14 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                     st = h.I2[v];
                     dv = D[v];
                 }
-                while (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+                if constexpr (BITS) {
+                    if (!placed) {
+                        h.sink_place(km, im, size, pK, pnode, pv, lane);
+                        placed = true;
+                    }
+                } else {
+                    while (!placed) placed = h.sink_round(head, hl, km, im, size, ldsLevel, lane);
+                }
                 xtick(1);
                 const double alt = mind + w;
                 int need = 0;
@@ -1379,11 +1538,14 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                     const int nk = __builtin_amdgcn_readlane(need, k);
                     const double ak = readlane_f64(alt, k);
                     if (nk == 1) {                    // igraph_2wheap_push_with_index
-                        h.shift_up(size, -ak, vk, lane);
+                        if constexpr (BITS) h.shift_up_bits(size, -ak, vk, size + 1, lane);
+                        else h.shift_up(size, -ak, vk, lane);
                         size += 1;
                     } else {                          // igraph_2wheap_modify (sink is a no-op)
                         const int p2 = moved ? h.I2[vk] : __builtin_amdgcn_readlane(st, k);
-                        h.shift_up(__builtin_amdgcn_readfirstlane(p2) - 2, -ak, vk, lane);
+                        const int pos = __builtin_amdgcn_readfirstlane(p2) - 2;
+                        if constexpr (BITS) h.shift_up_bits(pos, -ak, vk, size, lane);
+                        else h.shift_up(pos, -ak, vk, lane);
                     }
                     moved = true;
                 }
@@ -1839,6 +2001,10 @@ void launch_tie_write(const DevGraph& g, const DevTable& tab, const int32_t* dRo
 
 int exact_soa_max_n() { return EX_SOA_MAXN; }
 
+// LDS bytes of k_exact_rows' preferred-child bits: one bit per 1-based heap
+// node 0..n (16-B aligned)
+int exact_bits_bytes(int n) { return (int)((((size_t)n + 2 + 31) / 32 * 4 + 15) & ~(size_t)15); }
+
 void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                        const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc,
                        bool forceGlobalHeap, const int32_t* dSlots, const TieBuf& tie,
@@ -1854,18 +2020,25 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
                            dRows, nRows, dSlots, tie, dXdbg);
         return;
     }
-    const int bytes = (int)(((size_t)12 * hc + 15) & ~(size_t)15);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (dXdbg) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_rows<true>),
+    // the preferred-child bits follow the heap head when both fit (the
+    // engine sizes hc for them, exact_bits_bytes)
+    const int head = (int)(((size_t)12 * hc + 15) & ~(size_t)15);
+    const int withBits = head + exact_bits_bytes(g.n);
+    const bool bits = withBits <= 160 * 1024 - 512;
+    const int bytes = bits ? withBits : head;
+    auto go = [&](auto kern) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-        hipLaunchKernelGGL(k_exact_rows<true>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc,
-                           dRows, nRows, hc, dSlots, tie, dXdbg);
-        return;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc, dRows, nRows, hc,
+                           dSlots, tie, dXdbg);
+    };
+    if (dXdbg) {
+        if (bits) go(&k_exact_rows<true, true>);
+        else go(&k_exact_rows<true, false>);
+    } else {
+        if (bits) go(&k_exact_rows<false, true>);
+        else go(&k_exact_rows<false, false>);
     }
-    hipLaunchKernelGGL(k_exact_rows<false>, dim3(grid), dim3(EX_THREADS), bytes, st, g, tab, sc,
-                       dRows, nRows, hc, dSlots, tie, dXdbg);
 }
 
 void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,

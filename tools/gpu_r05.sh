@@ -89,8 +89,9 @@ for st in ${STAGES:-tests bench}; do
     done ;;
   hostfill)
     # the host_fill block alone (C4: rows path + fresh-engine fill_rowstore)
-    timeout -k 10 400 python3 -u bench.py --workload c4 --steps 3 --warmup 1 --no-cpu --tie-stress= --secondary= --d2h-rows 0 --no-stream > $OUT/hostfill.json 2> $OUT/hostfill.err || { tail -20 $OUT/hostfill.err; exit 1; }
-    python3 -c "import json; h=json.load(open('$OUT/hostfill.json'))['host_fill']; print({k: (round(v, 3) if isinstance(v, float) else v) for k, v in h.items() if k not in ('how', 'rows_path')}); print('rows_path', {k: (round(v, 3) if isinstance(v, float) else v) for k, v in h['rows_path'].items() if k != 'how'})" ;;
+    SHDPE_FILL_LOG=1 timeout -k 10 400 python3 -u bench.py --workload c4 --steps 3 --warmup 1 --no-cpu --tie-stress= --secondary= --d2h-rows 0 --no-stream > $OUT/hostfill.json 2> $OUT/hostfill.err || { tail -20 $OUT/hostfill.err; exit 1; }
+    python3 -c "import json; h=json.load(open('$OUT/hostfill.json'))['host_fill']; print({k: (round(v, 3) if isinstance(v, float) else v) for k, v in h.items() if k not in ('how', 'rows_path')}); print('rows_path', {k: (round(v, 3) if isinstance(v, float) else v) for k, v in h['rows_path'].items() if k != 'how'})"
+    grep "fill_rowstore" $OUT/hostfill.err || true ;;
   exactdbg)
     # k_exact_rows per-pop segment counters (SHDPE_DEBUG) on the c4q tie rows
     SHDPE_DEBUG=1 timeout -k 10 300 python3 -u bench.py --workload c4q --steps 1 --warmup 0 $QUICK > $OUT/exactdbg.json 2> $OUT/exactdbg.err || { tail -20 $OUT/exactdbg.err; exit 1; }
