@@ -290,15 +290,16 @@ static int configure(ShdPe* pe, Shard* sh) {
                   (tu.batch == 1 || (tu.batch != 0 && layout == 0) || pe->opt.forceMode == 5);
     BatchLaunch b{};
     // LB = 16 sources per batch; 8 when a shard has too few rows to give
-    // every resident workgroup (two per CU) a batch of 16.  C4 per-rank shard
-    // times (profiles/r04_shard_times.txt): N=4 (4,096 rows) LB 8 39.0 ms vs
-    // LB 16 42.7; N=8 (2,048 rows) LB 8 23.7 vs LB 16 39.5 vs LB 4 28.3 --
-    // LB 4 (32-B line pieces) stays a SHDPE_BATCH_LB option only.  (The
+    // every CU a batch of 16.  C4 per-rank shard times, same box: round 5
+    // (4-wave relax, one workgroup per CU; profiles/r05_ab_notes.txt r05w)
+    // N=4 (4,096 rows) LB 16 28.8 ms vs LB 8 31.0, N=8 (2,048 rows) LB 8 17.2
+    // vs LB 16 25.4; round 4 (two 8-wave workgroups per CU, r04_shard_times)
+    // had N=4 at LB 8.  LB 4 (32-B line pieces) stays a SHDPE_BATCH_LB option.  (The
     // round-4 cooperative relax -- K workgroups per batch -- and the post
     // kernel over lane slices are patches under tools/variants/)
     b.lb = tu.batchLB;
     if (b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32)
-        b.lb = ((int64_t)sh->rowCount + 15) / 16 >= 2 * (int64_t)sh->numCUs ? 16 : 8;
+        b.lb = ((int64_t)sh->rowCount + 15) / 16 >= (int64_t)sh->numCUs ? 16 : 8;
     b.threads = tu.batchThreads;
     if (b.threads != 256 && b.threads != 512) b.threads = 1024;
     // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
