@@ -45,7 +45,7 @@ extern "C" {
 #define SHD_PE_ENODEV       -3   /* no usable gfx950 device / HIP init failed     */
 #define SHD_PE_EUNREACHABLE -4   /* (per entry, see flags) target not reachable    */
 #define SHD_PE_ENOSELFLOOP  -5   /* (per entry, see flags) (s,s) self-loop missing */
-#define SHD_PE_EMULTI       -6   /* multigraph whose newest parallel edge between two vertices is not a fastest one (path latency would differ from the distance); other multigraphs are supported */
+#define SHD_PE_EMULTI       -6   /* reserved (before round 5: a multigraph whose newest parallel edge is not a fastest one; every multigraph is supported now) */
 #define SHD_PE_EHIP         -7   /* HIP runtime error during compute               */
 #define SHD_PE_ENOTATTACHED -8   /* vertex is not in the attached set              */
 #define SHD_PE_ENOEDGE      -9   /* direct path requested but (s,t) has no edge    */

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void k_self_paths(DevGraph g0, const int32_t* 
     for (int a = b + lane; a < e; a += 64) {
         const double L = g.lat[a];
         const int pos = (a - b) + ((self && a - b >= sp) ? 1 : 0);
-        if (L < bl || (L == bl && pos < bp)) { bl = L; bp = pos; br = g.rel[a]; }
+        if (L < bl || (L == bl && pos < bp)) { bl = L; bp = pos; br = g.srel ? g.srel[a] : g.rel[a]; }
     }
     if (lane == 0 && self) {
         const double L = g.selfMinLat[v];
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_pairs(DevGraph g0, const int32_t* __res
     double L = 0.0, R = 0.0;
     uint8_t f = F_NOEDGE;
     if (found) {
-        const double w = s == t ? g.selfLat[s] : g.lat[a];
+        const double w = s == t ? g.selfLat[s] : (g.flat ? g.flat[a] : g.lat[a]);   // get_eid: newest
         const double r = s == t ? g.selfRel[s] : g.rel[a];
         L = 0.0 + w;                                          // :1920
         R = acc * r;                                          // :1921

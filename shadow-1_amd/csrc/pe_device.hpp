@@ -55,6 +55,10 @@ struct DevGraph {
     const int32_t* attached;   // [T]
     const uint8_t* isAttached; // [n]
     const uint32_t* heavyBits; // [ceil(n/32)] vertices with degree >= heavyDeg
+    const double* flat;        // [nArcs] multigraphs with a slower newest parallel edge
+                               // (latFold) only, else null: the newest edge's latency
+                               // (path folds, direct paths; `lat` = group minimum)
+    const double* srel;        // [nArcs] latFold only: the self path's reliability
     const int32_t* oldId;      // [n] device id -> caller's vertex id (null: identity).
                                // The batched path relabels vertices by degree (rows
                                // keep igraph's incidence order); pred is mapped back
@@ -101,6 +105,7 @@ struct DevScratch {
     int64_t heapStride;  // heap tail entries per slot
     int32_t* index2;   // exact kernel: 0 never reached, 1 popped, >=2 heap pos+2
     int32_t* queue;    // sparse LAYOUT 3: frontier queues, (stride + hcap) per slot
+    double* lfold;     // latFold graphs only (else null): the folded latency label
     int64_t stride;    // elements per slot (>= n)
 };
 

@@ -206,7 +206,7 @@ extern "C" const char* shd_pe_strerror(int code) {
         case SHD_PE_ENODEV: return "no usable gfx950 device";
         case SHD_PE_EUNREACHABLE: return "target unreachable";
         case SHD_PE_ENOSELFLOOP: return "self-loop (s,s) missing";
-        case SHD_PE_EMULTI: return "multigraph whose newest parallel edge is not a fastest one (unsupported)";
+        case SHD_PE_EMULTI: return "multigraph error (reserved: no longer returned)";
         case SHD_PE_EHIP: return "HIP runtime error";
         case SHD_PE_ENOTATTACHED: return "vertex is not attached";
         case SHD_PE_ENOEDGE: return "no edge between the vertices";
@@ -493,7 +493,7 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
     // permuted host copies (only when relabelling)
     std::vector<int32_t> newOf, rp, ip;
     hvec<int32_t> col, o2i, icol;
-    hvec<double> lat, rel, ilat, irel;
+    hvec<double> lat, rel, ilat, irel, flt, srl;
     std::vector<double> vrel, sl, sr, sml, smr;
     std::vector<uint8_t> hs;
     std::vector<int32_t> att;
@@ -506,6 +506,7 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
         for (int32_t k = 0; k < n; ++k) rp[k + 1] = rp[k] + (g0.rowPtr[od[k] + 1] - g0.rowPtr[od[k]]);
         std::vector<int32_t> arcNew(m);
         col.resize(m); lat.resize(m); rel.resize(m); o2i.resize(m);
+        if (g0.latFold) { flt.resize(m); srl.resize(m); }
         for (int32_t k = 0; k < n; ++k) {
             const int32_t u = od[k];
             for (int32_t a = g0.rowPtr[u], j = rp[k]; a < g0.rowPtr[u + 1]; ++a, ++j) {
@@ -513,6 +514,7 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
                 col[j] = newOf[g0.col[a]];
                 lat[j] = g0.lat[a];
                 rel[j] = g0.rel[a];
+                if (g0.latFold) { flt[j] = g0.foldLat[a]; srl[j] = g0.selfPathRel[a]; }
             }
         }
         if (g0.directed) {
@@ -604,6 +606,15 @@ static int upload_graph(ShdPe* pe, Shard* sh, DevGraph* out, const std::vector<i
         d.inPtr = dip; d.inCol = dic; d.inLat = dil; d.inRel = dir;
     } else {
         d.inPtr = rowPtr; d.inCol = dcol; d.inLat = dlat; d.inRel = drel;
+    }
+    d.flat = d.srel = nullptr;
+    if (g0.latFold) {
+        double *dfl, *dsp;
+        if ((rc = dev_upload(sh, &dfl, perm ? flt : g0.foldLat)) ||
+            (rc = dev_upload(sh, &dsp, perm ? srl : g0.selfPathRel)))
+            return rc;
+        d.flat = dfl;
+        d.srel = dsp;
     }
     d.oldId = nullptr;
     if (perm) {
@@ -781,6 +792,12 @@ static int ensure_table(ShdPe* pe, Shard* sh) {
     sh->sc.heapStride = (int64_t)heapStride;
     sh->sc.index2 = (int32_t*)i2;
     sh->sc.stride = (int64_t)stride;
+    sh->sc.lfold = nullptr;
+    if (pe->hg.latFold) {
+        void* lf;
+        if ((rc = dev_alloc(sh, &lf, slots * stride * 8))) return rc;
+        sh->sc.lfold = (double*)lf;
+    }
     if (!pe->batched && (sh->cfg.layout == 3 || sh->cfg.layout == 0)) {
         void* q;
         const size_t per = 2 * ((size_t)sh->cfg.qcap + sh->cfg.hcap);
@@ -1049,7 +1066,10 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
             HIPCHK(hipEventSynchronize(sh->evB));
             st.msDirectKernel += elapsed(sh->evA, sh->evB);
             st.launchesDirect++;
-        } else if (pe->opt.forceMode == 3) {
+        } else if (pe->opt.forceMode == 3 || pe->hg.latFold) {
+            // (latFold multigraphs: the reported latency is a fold of other
+            // edges' latencies than the distance's -- the exact emulation
+            // carries it as a label, so every row takes that path)
             exactRows.assign(pos + c0, pos + c0 + cnt);
         } else if (pe->mode == 3) {
             if ((rc = ensure_dense(pe, sh))) return rc;
@@ -1237,7 +1257,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 dSl = sh->dSlots;
                 while (nTie < (int32_t)exactSlots.size() && exactSlots[nTie] >= 0) ++nTie;
             }
-            const bool dense = pe->mode == 3 && pe->opt.forceMode != 3 && !dSl;
+            const bool dense = pe->mode == 3 && pe->opt.forceMode != 3 && !pe->hg.latFold && !dSl;
             if (dense && !sh->dXList &&
                 (rc = dev_alloc(sh, &sh->dXList, (size_t)sh->exactGrid * (size_t)sh->sc.stride *
                                                      (size_t)exact_dense_list_bytes())))

@@ -17,10 +17,16 @@
 // parent vertex as one relaxation by min(w) (a second shift_up continues the
 // first over the same ancestor chain), so a group of parallel edges becomes
 // ONE arc with the group's minimum latency and the newest edge's reliability.
-// The path latency the reference reports is the fold of get_eid latencies,
-// which equals the Dijkstra distance only when the newest edge of every group
-// is a fastest one; other multigraphs are rejected (SHD_PE_EMULTI).  Several
-// self-loops on a vertex: the same rule (the newest one is the (v, v) edge).
+// The path latency the reference reports is the fold of get_eid latencies
+// (topology.c:1488-1498), which equals the Dijkstra distance when the newest
+// edge of every group is a fastest one.  When some group's newest edge is
+// slower (HostGraph::latFold), the merged arc keeps the group MINIMUM for the
+// relaxations, `foldLat` the newest edge's latency for the path folds and
+// direct paths, and `selfPathRel` the reliability of the edge the self path's
+// strict-'<' scan of v's incident edges settles on (the newest of the
+// group's fastest edges: igraph lists parallel edges newest first); the
+// engine then computes such graphs' rows with the exact emulation, which
+// folds the latency label along the path like the reference.
 #include "pe_graph.hpp"
 
 #include <algorithm>
@@ -103,11 +109,30 @@ static bool sort_rows(int32_t n, const std::vector<int32_t>& ptr, hvec<int32_t>&
     return false;
 }
 
-// One arc per (vertex, neighbour): the newest parallel edge (the last of its
-// group in edge-id order) with the group's minimum latency, which must be the
-// newest edge's own (see the header); rows compacted in place.
-static int merge_parallel(int32_t n, std::vector<int32_t>& ptr, hvec<int32_t>& colv, hvec<double>& latv,
-                          hvec<double>& relv) {
+// One arc per (vertex, neighbour): the group's minimum latency, the newest
+// parallel edge's (the last of its group in edge-id order) reliability; for
+// latFold graphs also the newest edge's latency and the self path's
+// reliability (see the header); rows compacted in place.
+static int merge_parallel(HostGraph* g) {
+    const int32_t n = g->n;
+    std::vector<int32_t>& ptr = g->rowPtr;
+    hvec<int32_t>& colv = g->col;
+    hvec<double>& latv = g->lat;
+    hvec<double>& relv = g->rel;
+    bool fold = false;
+    for (int32_t v = 0; v < n && !fold; ++v)
+        for (int32_t a = ptr[v]; a < ptr[v + 1];) {
+            int32_t z = a + 1;
+            double mn = latv[a];
+            while (z < ptr[v + 1] && colv[z] == colv[a]) { mn = std::min(mn, latv[z]); ++z; }
+            if (latv[z - 1] != mn) fold = true;
+            a = z;
+        }
+    g->latFold = fold;
+    if (fold) {
+        g->foldLat.resize(colv.size());
+        g->selfPathRel.resize(colv.size());
+    }
     int32_t w = 0;
     for (int32_t v = 0; v < n; ++v) {
         const int32_t b = ptr[v], e = ptr[v + 1];
@@ -115,11 +140,18 @@ static int merge_parallel(int32_t n, std::vector<int32_t>& ptr, hvec<int32_t>& c
         for (int32_t a = b; a < e;) {
             int32_t z = a + 1;
             double mn = latv[a];
-            while (z < e && colv[z] == colv[a]) { mn = std::min(mn, latv[z]); ++z; }
+            int32_t lastMin = a;
+            while (z < e && colv[z] == colv[a]) {
+                if (latv[z] <= mn) { mn = latv[z]; lastMin = z; }
+                ++z;
+            }
             const int32_t newest = z - 1;
-            if (latv[newest] != mn) return SHD_PE_EMULTI;
+            if (fold) {
+                g->foldLat[w] = latv[newest];
+                g->selfPathRel[w] = relv[lastMin];
+            }
             colv[w] = colv[newest];
-            latv[w] = latv[newest];
+            latv[w] = mn;
             relv[w] = relv[newest];
             ++w;
             a = z;
@@ -129,6 +161,10 @@ static int merge_parallel(int32_t n, std::vector<int32_t>& ptr, hvec<int32_t>& c
     colv.resize(w);
     latv.resize(w);
     relv.resize(w);
+    if (fold) {
+        g->foldLat.resize(w);
+        g->selfPathRel.resize(w);
+    }
     return SHD_PE_OK;
 }
 
@@ -244,7 +280,7 @@ int build_host_graph(const ShdPeGraphDesc* d, HostGraph* g) {
     if (sort_rows(n, g->rowPtr, g->col, g->lat, g->rel)) {
         rawDeg.resize(n);
         for (int32_t v = 0; v < n; ++v) rawDeg[v] = g->rowPtr[v + 1] - g->rowPtr[v];
-        const int rc = merge_parallel(n, g->rowPtr, g->col, g->lat, g->rel);
+        const int rc = merge_parallel(g);
         if (rc) return rc;
     }
     const int64_t nArcsM = g->rowPtr[n];
@@ -323,7 +359,7 @@ int host_direct_path(const HostGraph& g, int32_t s, int32_t t, double* lat, doub
     const int64_t a = g.findArc(s, t);
     double L, R;
     if (a == -2) { L = g.selfLat[s]; R = g.selfRel[s]; }
-    else if (a >= 0) { L = g.lat[a]; R = g.rel[a]; }
+    else if (a >= 0) { L = g.latFold ? g.foldLat[a] : g.lat[a]; R = g.rel[a]; }   // get_eid: the newest
     else return SHD_PE_ENOEDGE;
     totalLatency += L;                              // :1920
     totalReliability *= R;                          // :1921
@@ -344,9 +380,10 @@ int host_self_path(const HostGraph& g, int32_t v, double* lat, double* rel) {
     };
     const int32_t b = g.rowPtr[v], e = g.rowPtr[v + 1];
     int32_t a = b;
-    for (; a < e && g.col[a] < v; ++a) visit(g.lat[a], g.rel[a]);
+    const double* srel = g.latFold ? g.selfPathRel.data() : g.rel.data();
+    for (; a < e && g.col[a] < v; ++a) visit(g.lat[a], srel[a]);
     if (g.hasSelf[v]) visit(g.selfMinLat[v], g.selfMinRel[v]);
-    for (; a < e; ++a) visit(g.lat[a], g.rel[a]);
+    for (; a < e; ++a) visit(g.lat[a], srel[a]);
     if (!any && g.nEdges == 0) return SHD_PE_ENOEDGE;
     if (lat) *lat = 2.0 * minLatency;               // :1640
     if (rel) *rel = relMin * relMin;                // :1641

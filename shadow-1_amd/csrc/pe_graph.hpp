@@ -40,6 +40,11 @@ struct HostGraph {
     hvec<int32_t> inCol;
     hvec<double> inLat, inRel;
     hvec<int32_t> outToIn;
+    // multigraphs whose newest parallel edge is not a fastest one (latFold):
+    // per merged OUT arc the newest edge's latency (path folds, direct paths;
+    // `lat` holds the group minimum) and the self path's reliability
+    bool latFold = false;
+    hvec<double> foldLat, selfPathRel;
     // vertex data
     std::vector<double> vrel;       // 1 - packetloss, 1.0 when absent/NaN
     std::vector<double> selfLat, selfRel;        // newest self-loop: igraph_get_eid(v, v)

@@ -1408,6 +1408,10 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
     int32_t* H = sc.hops + slot;
     double* R = sc.rel + slot;
     int32_t* P = sc.pred + slot;
+    // latFold multigraphs (g.flat): the reported latency is the fold of the
+    // newest parallel edges' latencies along the path (topology.c:1488-1498),
+    // a third label beside hops and reliability
+    double* LF = g.flat && sc.lfold ? sc.lfold + slot : nullptr;
     double* tailKey = reinterpret_cast<double*>(sc.heapTail) + (size_t)blockIdx.x * 2 * sc.heapStride;
     const WHeap h{tailKey, reinterpret_cast<int32_t*>(tailKey + sc.heapStride), sc.index2 + slot, hc,
                   reinterpret_cast<uint32_t*>(ex_smem + (((size_t)12 * hc + 15) & ~(size_t)15))};
@@ -1436,6 +1440,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
             H[s] = 0;
             R[s] = 1.0;
             P[s] = -1;
+            if (LF) LF[s] = 0.0;
         }
         __syncthreads();
         int toReach = g.T;
@@ -1461,8 +1466,9 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
             const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
             const int att = g.isAttached[u];
             int hu = 0;
-            double ru = 1.0;
+            double ru = 1.0, lfu = 0.0;
             if (labels) { hu = H[u]; ru = R[u]; }
+            if (labels && LF) lfu = LF[u];
             size -= 1;
             double km = 0.0;
             int im = 0;
@@ -1526,6 +1532,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                     P[v] = ia;
                     D[v] = alt;
                     if (labels) { H[v] = hu + 1; R[v] = ru * g.rel[a]; }
+                    if (labels && LF) LF[v] = lfu + g.flat[a];
                 }
                 unsigned long long mask = __ballot(need != 0);
                 xtick(2);
@@ -1562,7 +1569,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows(DevGraph g0, DevTable
                          [&](int v) { return thr >= 0.0 && h.I2[v] == 1; }, D, P);
         else
             write_row(g, tab, r, s,
-                      [&](int t) { return h.I2[t] == 1 ? d2b(D[t]) : INF_BITS; },
+                      [&](int t) { return h.I2[t] == 1 ? d2b(LF ? LF[t] : D[t]) : INF_BITS; },
                       [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
         __syncthreads();
     }
@@ -1597,6 +1604,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
     int32_t* H = sc.hops + slot;
     double* R = sc.rel + slot;
     int32_t* P = sc.pred + slot;
+    double* LF = g.flat && sc.lfold ? sc.lfold + slot : nullptr;   // latFold (k_exact_rows)
     {
         const size_t m = (size_t)g.rowPtr[n];
         uint32_t acc = warm_cache(g.rowPtr, (size_t)4 * (n + 1), lane, EX_THREADS);
@@ -1649,6 +1657,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
             H[s] = 0;
             R[s] = 1.0;
             P[s] = -1;
+            if (LF) LF[s] = 0.0;
         }
         __syncthreads();
         int size = tslot >= 0 && thr < 0.0 ? 0 : 1;   // uniform; 0: relevance scan cleared the row
@@ -1666,6 +1675,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
             const int att = g.isAttached[u];
             const int hu = H[u];
             const double ru = R[u];
+            const double lfu = LF ? LF[u] : 0.0;
             size -= 1;
             if (lane == 0) {
                 if (size > 0) {
@@ -1694,6 +1704,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
                 const int nh = hu + 1;
                 const double nr = ru * rw;
                 if (need) { P[v] = ia; H[v] = nh; R[v] = nr; }
+                if (need && LF) LF[v] = lfu + g.flat[ac];
                 unsigned long long mask = __ballot(need != 0);
                 while (mask) {
                     const int k = __builtin_ctzll(mask);
@@ -1719,7 +1730,7 @@ __global__ __launch_bounds__(EX_THREADS) void k_exact_rows_soa(DevGraph g0, DevT
                          [&](int v) { return thr >= 0.0 && index2[v] == 1; }, D, P);
         else
             write_row(g, tab, r, s,
-                      [&](int t) { return index2[t] == 1 ? d2b(D[t]) : INF_BITS; },
+                      [&](int t) { return index2[t] == 1 ? d2b(LF ? LF[t] : D[t]) : INF_BITS; },
                       [&](int t) { return H[t]; }, R, P, F_EXACT, lane, EX_THREADS);
         __syncthreads();
     }
@@ -1925,7 +1936,7 @@ __global__ __launch_bounds__(256) void k_direct_rows(DevGraph g0, DevTable tab0,
             }
             if (lo < a1 && g.col[lo] == t) a = lo;
         }
-        if (a >= 0) { L = 0.0 + g.lat[a]; Rl = acc * g.rel[a]; h = 1; }
+        if (a >= 0) { L = 0.0 + (g.flat ? g.flat[a] : g.lat[a]); Rl = acc * g.rel[a]; h = 1; }
         else f |= F_NOEDGE;
     }
     const size_t idx = (size_t)(r - tab.rowStart) * (size_t)tab.T + j;

@@ -198,6 +198,34 @@ def minus_one_edge(top: Topology, seed: int = 0) -> Topology:
                     name=top.name + "_minus1")
 
 
+def with_slower_newest_edges(top: Topology, frac: float, seed: int) -> Topology:
+    """A multigraph where many groups' NEWEST parallel edge (igraph_get_eid's,
+    the one the reference folds, topology.c:1488-1498) is SLOWER than an older
+    one: copies of a fraction of the non-loop edges appended after the
+    originals, half of them slower (x1.1-2.5), half faster, some groups of
+    three; the reported latency is then the fold of the newest edges'
+    latencies along the Dijkstra path, not the distance."""
+    rng = np.random.default_rng(seed)
+    cand = np.flatnonzero(top.src != top.dst)
+    pick = rng.choice(cand, size=max(1, int(frac * cand.shape[0])), replace=False)
+    src, dst, lat, loss = [top.src], [top.dst], [top.latency], [top.loss]
+    for rep in range(2):
+        sel = pick if rep == 0 else pick[rng.random(pick.shape[0]) < 0.3]
+        slower = rng.random(sel.shape[0]) < 0.5
+        l = top.latency[sel] * np.where(slower, rng.uniform(1.1, 2.5, sel.shape[0]),
+                                        rng.uniform(0.4, 0.95, sel.shape[0]))
+        if not top.directed:
+            flip = rng.random(sel.shape[0]) < 0.5
+            src.append(np.where(flip, top.dst[sel], top.src[sel]))
+            dst.append(np.where(flip, top.src[sel], top.dst[sel]))
+        else:
+            src.append(top.src[sel]); dst.append(top.dst[sel])
+        lat.append(l); loss.append(rng.uniform(0.0, 0.05, size=sel.shape[0]))
+    return Topology(n=top.n, directed=top.directed, src=np.concatenate(src), dst=np.concatenate(dst),
+                    latency=np.concatenate(lat), loss=np.concatenate(loss), vloss=top.vloss,
+                    name=top.name + "_slow_newest")
+
+
 def with_parallel_edges(top: Topology, frac: float, seed: int, consistent: bool = True,
                         loops: bool = True) -> Topology:
     """A multigraph: parallel copies of a fraction of the edges (and of the
@@ -205,7 +233,7 @@ def with_parallel_edges(top: Topology, frac: float, seed: int, consistent: bool 
     of its group -- the one igraph_get_eid returns (oracle orc_get_eid).  With
     `consistent` every copy is also a fastest edge of its group (equal latency
     with another loss, or faster); otherwise one copy is slower than the edge
-    it duplicates (the engine rejects that, SHD_PE_EMULTI)."""
+    it duplicates (see with_slower_newest_edges)."""
     rng = np.random.default_rng(seed)
     cand = np.flatnonzero(top.src != top.dst)
     if loops:

@@ -47,6 +47,8 @@ def _graphs():
     yield "multigraph_directed", G.with_parallel_edges(G.random_sparse(400, 6, seed=13, directed=True), 0.3, seed=6)
     yield "parallel_loops", G.with_parallel_loops(G.random_sparse(400, 6, seed=14, quantum=5.0), 0.6, seed=8)
     yield "parallel_loops_directed", G.with_parallel_loops(G.random_sparse(300, 6, seed=15, directed=True), 0.6, seed=9)
+    yield "newest_slower", G.with_slower_newest_edges(G.random_sparse(400, 6, seed=16, quantum=5.0), 0.4, seed=12)
+    yield "newest_slower_directed", G.with_slower_newest_edges(G.random_sparse(300, 6, seed=17, directed=True), 0.4, seed=13)
 
 
 @pytest.mark.parametrize("name,top", list(_graphs()), ids=[n for n, _ in _graphs()])

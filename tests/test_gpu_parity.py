@@ -211,15 +211,65 @@ def test_complete_graph_direct_rows(E, oracle_mod):
     eng.close()
 
 
-def test_multigraph_rejected(E):
-    """The newest parallel edge (igraph_get_eid's, the one the reference folds)
-    slower than an older one: the table's latency would differ from the
-    distance -- rejected."""
+def test_multigraph_newest_slower_small(E, oracle_mod):
+    """The newest parallel edge (igraph_get_eid's, the one the reference
+    folds, topology.c:1488-1498) slower than an older one: Dijkstra runs on
+    the faster edge, the reported latency folds the newest one's -- row
+    latency 2.0 over a distance of 1.0 (was rejected with EMULTI before
+    round 5)."""
     top = Topology(3, False, np.array([0, 1, 0, 0, 1, 2]), np.array([1, 0, 0, 2, 1, 2]),
                    np.array([1.0, 2.0, 1.0, 1.0, 1.0, 1.0]), np.zeros(6))
-    with pytest.raises(E.EngineError) as ei:
-        E.Engine(top, np.arange(3))
-    assert ei.value.code == E.EMULTI
+    _check_engine(E, oracle_mod, top, np.arange(3))
+    eng = E.Engine(top, np.arange(3))
+    eng.compute_all()
+    assert eng.get_row(0)["lat"][1] == 2.0
+    eng.close()
+
+
+@pytest.mark.parametrize("directed", [False, True], ids=["undirected", "directed"])
+@pytest.mark.parametrize("quantum", [0.0, 10.0], ids=["tiefree", "quantised"])
+@pytest.mark.parametrize("force", [0, 5], ids=["sparse", "batched"])
+def test_multigraph_newest_slower_rows(E, oracle_mod, directed, quantum, force):
+    """Multigraphs where half of the parallel groups' newest edge is the
+    slower one (HostGraph::latFold): every row through the exact emulation
+    with the folded-latency label, bit-exact against the oracle's igraph run
+    over the unmerged edge list (n = 400: the all-LDS heap kernel)."""
+    base = G.random_sparse(400, 5, seed=51 + int(directed), directed=directed, quantum=quantum, vloss=True)
+    top = G.with_slower_newest_edges(base, 0.3, seed=9)
+    st = _check_engine(E, oracle_mod, top, np.arange(0, 400, 3, dtype=np.int32), force=force)
+    assert st["rowsExact"] > 0
+
+
+@pytest.mark.parametrize("hc", [0, 64], ids=["lds_head", "global_tail"])
+def test_multigraph_newest_slower_large(E, oracle_mod, monkeypatch, hc):
+    """The same on n = 12,000 (k_exact_rows: the preferred-child-bit heap;
+    with SHDPE_EXACT_HC=64 the heap lives almost wholly in the global tail)."""
+    dbg = 0
+    if hc:
+        monkeypatch.setenv("SHDPE_EXACT_HC", str(hc))
+        dbg = E.DEBUG_ENV
+    top = G.with_slower_newest_edges(G.random_sparse(12000, 5, seed=61, quantum=10.0), 0.2, seed=10)
+    _check_engine(E, oracle_mod, top, np.arange(0, 12000, 500, dtype=np.int32),
+                  sources=np.arange(0, 12000, 1000, dtype=np.int32), debug_flags=dbg)
+
+
+def test_multigraph_newest_slower_complete(E, oracle_mod):
+    """A complete multigraph (direct rows, topology.c:1877-1927): the direct
+    path reads igraph_get_eid's edge, the newest parallel one."""
+    base = G.dense(40, seed=5)
+    top = G.with_slower_newest_edges(base, 0.3, seed=11)
+    og = oracle_mod.OracleGraph(top)
+    eng = E.Engine(top, np.arange(top.n))
+    assert eng.is_complete
+    eng.compute_all()
+    for s in range(top.n):
+        r = eng.get_row(s)
+        assert np.all(r["flags"] == E.F_DIRECT)
+        for t in range(top.n):
+            lat, rel = og.direct(s, t)
+            assert r["lat"][t] == lat and r["rel"][t] == rel, (s, t)
+    assert eng.stats()["mode"] == 2
+    eng.close()
 
 
 @pytest.mark.parametrize("directed", [False, True], ids=["undirected", "directed"])

@@ -63,16 +63,16 @@ def test_engine_fails_loudly_without_gpu(lib):
 
 
 def test_multigraph_host_build_without_gpu(lib):
-    """The host graph build runs before the device check: a multigraph whose
-    newest parallel edge is a fastest one of its group is accepted (the create
-    then stops at ENODEV on this GPU-less box), one whose newest parallel edge
-    -- igraph_get_eid's edge, the one the reference folds -- is slower than
-    another is rejected with EMULTI (edges); parallel self-loops in any
-    latency order are accepted (a loop never changes a distance)."""
+    """The host graph build runs before the device check: every multigraph
+    is accepted (the create then stops at ENODEV on this GPU-less box) --
+    those whose newest parallel edge is a fastest one of its group, those
+    whose newest edge (igraph_get_eid's, the one the reference folds) is
+    slower than another (round 5: the exact emulation folds that edge's
+    latency along the path), and parallel self-loops in any latency order."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present")
-    from shdpe.engine import Engine, EngineError, ENODEV, EMULTI
+    from shdpe.engine import Engine, EngineError, ENODEV
     from shdpe.graph import Topology
     base = G.random_sparse(60, 4, seed=2)
     for directed in (False, True):
@@ -82,7 +82,10 @@ def test_multigraph_host_build_without_gpu(lib):
         assert ei.value.code == ENODEV
         with pytest.raises(EngineError) as ei:
             Engine(G.with_parallel_edges(b, 0.4, seed=3, consistent=False, loops=False), np.arange(60))
-        assert ei.value.code == EMULTI
+        assert ei.value.code == ENODEV
+        with pytest.raises(EngineError) as ei:
+            Engine(G.with_slower_newest_edges(b, 0.4, seed=4), np.arange(60))
+        assert ei.value.code == ENODEV
     # two self-loops on vertex 0, the newer one slower: accepted
     top = Topology(base.n, False, np.concatenate([base.src, [0]]), np.concatenate([base.dst, [0]]),
                    np.concatenate([base.latency, [base.latency[base.src == base.dst][0] + 1.0]]),
