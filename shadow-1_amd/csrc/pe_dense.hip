@@ -96,8 +96,13 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
     __shared__ uint16_t actList[MAXCH];
     const int tid = threadIdx.x;
     const int tx = tid & 15, ty = tid >> 4;
-    const int64_t v0 = (int64_t)blockIdx.x * TCOL;
-    const int r0 = blockIdx.y * TR;
+    // row tiles vary fastest over the grid: the workgroups dispatched together
+    // (round-robin over the XCDs) read the same W column strip, so a K chunk of
+    // W is fetched from HBM once per XCD and served from L2 to the other row
+    // tiles, instead of once per row tile
+    const int rowTile = blockIdx.x;
+    const int64_t v0 = (int64_t)blockIdx.y * TCOL;
+    const int r0 = rowTile * TR;
     const double* __restrict__ Wg = dglobal(W);
     double* Dg = dglobal(D);
     if (MODE == MP_SWEEP) {
@@ -117,7 +122,7 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
     if (useList) {
         if (tid == 0) nAct = 0;
         __syncthreads();
-        const uint8_t* ce = dglobal(chunkEpoch) + (size_t)blockIdx.y * nch;
+        const uint8_t* ce = dglobal(chunkEpoch) + (size_t)rowTile * nch;
         for (int c = tid; c < nch; c += 256)
             if ((int)ce[c] >= epoch - 1) actList[atomicAdd(&nAct, 1)] = (uint16_t)c;
         __syncthreads();
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
             if (rowCh) { dglobal(rowChanged)[r] = 1; changed += rowCh; }
         }
         if (epoch > 0 && colCh) {
-            uint8_t* ce = dglobal(chunkEpoch) + (size_t)blockIdx.y * nch + (v0 / KB);
+            uint8_t* ce = dglobal(chunkEpoch) + (size_t)rowTile * nch + (v0 / KB);
 #pragma unroll
             for (int j = 0; j < MJ; ++j)
                 if ((colCh >> j) & 1) ce[j] = (uint8_t)epoch;
@@ -354,16 +359,16 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
                        W, D, dRows, n, ldD, rowActive);
     (void)hipMemsetAsync(rowAmb, 0, nRows, st);
     const unsigned gx = (unsigned)((n + TCOL - 1) / TCOL);
-    const dim3 gridS(gx, (unsigned)((nRows + 16 * MI_SWEEP - 1) / (16 * MI_SWEEP)));
-    const int miP = tu.densePredMi == 2 ? 2 : MI_PRED;
-    const dim3 gridP(gx, (unsigned)((nRows + 16 * miP - 1) / (16 * miP)));
+    const dim3 gridS((unsigned)((nRows + 16 * MI_SWEEP - 1) / (16 * MI_SWEEP)), gx);
+    const int miP = tu.densePredMi == 4 || tu.densePredMi == 6 ? tu.densePredMi : MI_PRED;
+    const dim3 gridP((unsigned)((nRows + 16 * miP - 1) / (16 * miP)), gx);
     // chunk epochs (uint8): sweep t visits chunks changed at t-1 or t; the
     // initial rows count as changed at epoch 0.  Off beyond 250 sweeps or
     // when the chunk list would not fit.
     const int64_t nch = (n + KB - 1) / KB;
     const bool epochs = nch <= MAXCH && tu.denseEpochs;
     if (epochs)
-        (void)hipMemsetAsync(chunkEpoch, 0, (size_t)gridS.y * (size_t)nch, st);
+        (void)hipMemsetAsync(chunkEpoch, 0, (size_t)gridS.x * (size_t)nch, st);
     int sweeps = 0;
     double visits = 0.0;
     for (;; ++sweeps) {
@@ -391,8 +396,11 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
         }
         if (!any || sweeps > n) break;
     }
-    if (miP == 2)
-        hipLaunchKernelGGL((k_minplus<MP_PRED, 2>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
+    if (miP == 6)
+        hipLaunchKernelGGL((k_minplus<MP_PRED, 6>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
+                           rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
+    else if (miP == 4)
+        hipLaunchKernelGGL((k_minplus<MP_PRED, 4>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
                            rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
     else
         hipLaunchKernelGGL((k_minplus<MP_PRED, MI_PRED>), gridP, dim3(256), 0, st, g, W, D, n, ldD,
