@@ -117,7 +117,8 @@ struct ShdPe {
     std::vector<std::unique_ptr<Shard>> shards;
     std::unique_ptr<std::atomic<uint8_t>[]> rowDone;
     bool gathered = false;
-    int64_t putRows = 0;             // rows imported by shd_pe_put_rows (host transport)
+    int64_t putRows = 0;             // distinct rows imported by shd_pe_put_rows (host transport)
+    std::vector<uint8_t> putSeen;    // per table row: imported already (a repeated put counts once)
     bool putInit = false;            // own shard rows copied into the full table
     ncclComm_t xcomm = nullptr;      // cross-process communicator (shd_pe_comm_init)
     int32_t ownStart = 0, ownEnd = 0;
@@ -1798,6 +1799,7 @@ struct HostImage {
     size_t bytes = 0;
     bool registered = false;
     double msTouch = 0.0, msRegister = 0.0;
+    ~HostImage();
 };
 
 static void host_image_prepare(HostImage* im, size_t bytes) {
@@ -1829,11 +1831,11 @@ static void host_image_release(HostImage* im) {
     im->p = nullptr;
 }
 
+HostImage::~HostImage() { host_image_release(this); }   // every exit path of fill_rowstore
+
 static void host_image_free_cb(void* ctx, void* p) {
-    HostImage* im = static_cast<HostImage*>(ctx);
     (void)p;
-    host_image_release(im);
-    delete im;
+    delete static_cast<HostImage*>(ctx);
 }
 
 extern "C" int shd_pe_fill_rowstore(ShdPe* pe, ShdRowStore* st, int32_t* rowResult, double* msOut) {
@@ -1857,7 +1859,7 @@ extern "C" int shd_pe_fill_rowstore(ShdPe* pe, ShdRowStore* st, int32_t* rowResu
         std::fprintf(stderr, "[shdpe] fill_rowstore: compute %.1f ms, image %.2f GB touch %.1f ms + "
                      "register %.1f ms (%s), join wait %.1f ms\n", ms(t0, tc), bytes / 1e9, him->msTouch,
                      him->msRegister, him->registered ? "registered" : "NOT registered", ms(tc, now()));
-    if (rc) { host_image_release(him.get()); return rc; }
+    if (rc) return rc;
     if (pack && !him->p) return SHD_PE_ENOMEM;
     std::lock_guard<std::mutex> lk(pe->copyMu);
     const DevTable* tab = nullptr;
@@ -1865,17 +1867,15 @@ extern "C" int shd_pe_fill_rowstore(ShdPe* pe, ShdRowStore* st, int32_t* rowResu
     if (pe->gathered) tab = &s->full;
     else if (pe->G == 1) tab = &s->tab;
     else return SHD_PE_ENOTOWNED;          // rows spread over shards: gather first
-    if (hipSetDevice(s->device) != hipSuccess) { host_image_release(him.get()); return SHD_PE_EHIP; }
+    if (hipSetDevice(s->device) != hipSuccess) return SHD_PE_EHIP;
     void *dImg = nullptr, *dOff = nullptr, *dAcc = nullptr, *dAll = nullptr;
     void* const hImg = him->p;
-    struct Free {   // device temporaries (and the host image until adopted), every exit path
+    struct Free {   // device temporaries, every exit path (the host image: ~HostImage)
         void** p[4];
-        std::unique_ptr<HostImage>* h;
         ~Free() {
             for (void** q : p) if (*q) (void)hipFree(*q);
-            if (*h) host_image_release(h->get());
         }
-    } fr{{&dImg, &dOff, &dAcc, &dAll}, &him};
+    } fr{{&dImg, &dOff, &dAcc, &dAll}};
     if ((pack && hipMalloc(&dImg, bytes) != hipSuccess) ||
         hipMalloc(&dOff, off.size() * 8) != hipSuccess || hipMalloc(&dAcc, 16) != hipSuccess ||
         hipMalloc(&dAll, (size_t)T * 4) != hipSuccess)
@@ -2118,7 +2118,9 @@ extern "C" int shd_pe_put_rows(ShdPe* pe, int32_t start, int32_t count, const do
     if (pe->opt.storePred)
         HIPCHK(hipMemcpyAsync(s->full.pred + o, pred, cells * 4, hipMemcpyHostToDevice, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
-    pe->putRows += count;
+    if (pe->putSeen.empty()) pe->putSeen.assign(ts, 0);
+    for (int32_t p = start; p < start + count; ++p)
+        if (!pe->putSeen[(size_t)p]) { pe->putSeen[(size_t)p] = 1; ++pe->putRows; }
     if (pe->putRows + (pe->ownEnd - pe->ownStart) >= (int64_t)ts) {
         for (size_t p = 0; p < ts; ++p) pe->rowDone[p].store(1, std::memory_order_release);
         pe->gathered = true;
