@@ -157,3 +157,29 @@ def test_fill_rowstore_equals_store_rows(E, name, top, force):
     st.close()
     ref.close()
     eng.close()
+
+
+def test_fill_rowstore_sharded_engine(E):
+    """A multi-shard engine (logical shards on the test GPU) refuses the
+    one-call fill with SHD_PE_ENOTOWNED until its rows are gathered (its
+    host image is released on that path), then fills exactly as a
+    one-shard engine does."""
+    top = G.power_law(6_000, m=3, seed=25)
+    att = G.sample_attached(top.n, 700, seed=4)
+    one = E.Engine(top, att, force_mode=5)
+    ref = E.RowStore(top.n, one.attached)
+    rr, _ = one.fill_rowstore(ref)
+    eng = E.Engine(top, att, force_mode=5, devices=[0, 0])
+    st = E.RowStore(top.n, eng.attached)
+    for _ in range(2):                              # (a repeat must not leak or crash)
+        with pytest.raises(E.EngineError) as ei:
+            eng.fill_rowstore(st)
+        assert ei.value.code == E.ENOTOWNED
+    assert st.size() == 0
+    eng.gather()
+    res, _ = eng.fill_rowstore(st)
+    assert np.array_equal(res, rr)
+    assert st.size() == ref.size() and st.min_latency() == ref.min_latency()
+    assert sorted(st.items()) == sorted(ref.items())
+    for x in (st, ref, eng, one):
+        x.close()
