@@ -1430,10 +1430,39 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
             if (perPart ? part[k][1] < part[pk][1] : ms[k] < ms[pk]) pk = k;
         }
         if (!perPart) pk = rk;
-        sh->bcfg = cand[rk];
+        // bucket width: the chosen relax variant once more at 0.8 x delta,
+        // kept if its relax kernel is faster on this shard (C4 same box: N=1
+        // -1.2%, the N=8 shard's LB-8 batches -2%; C5 +1.2%, so not a fixed
+        // default; profiles/r05_ab_notes.txt r05bg-bi).  The post kernel does
+        // not use delta.
+        BatchLaunch relaxPick = cand[rk];
+        double relaxAlt = 0.0;
+        if (perPart) {
+            BatchLaunch alt = cand[rk];
+            alt.delta = cand[rk].delta * 0.8;
+            sh->bcfg = alt;
+            sh->bcfgPost = cand[pk];
+            for (int rep = 0; rep < 2; ++rep) {
+                sh->msPart[0] = sh->msPart[1] = 0.0;
+                sh->timeParts = rep == 1;
+                const int rc = compute_shard(pe, sh, pos.data(), sh->rowCount);
+                sh->timeParts = false;
+                if (rc) {
+                    sh->bcfg = orig[0]; sh->bcfgAlt = orig[1]; sh->bcfgAlt2 = orig[2];
+                    sh->bcfgPost = BatchLaunch{};
+                    sh->stats = keep;
+                    return rc;
+                }
+            }
+            relaxAlt = sh->msPart[0];
+            if (relaxAlt > 0.0 && relaxAlt < part[rk][0]) relaxPick = alt;
+            sh->bcfgPost = BatchLaunch{};
+        }
+        sh->bcfg = relaxPick;
         if (pk != rk) sh->bcfgPost = cand[pk];
         sh->tuned = true;
         sh->stats = keep;
+        sh->stats.deltaUsed = relaxPick.delta;
         sh->stats.batchWaves = sh->bcfg.wpe;
         sh->stats.batchPostWaves = sh->bcfg.split ? cand[pk].wpe : 0;
         if (pe->tu.debug || pe->tu.tuneLog)
@@ -1441,6 +1470,9 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
                 std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms (relax %.2f post %.2f)%s\n",
                              sh->gindex, w[k], ms[k], part[k][0], part[k][1],
                              k == nc - 1 ? (pk == rk ? " -> one variant" : " -> per part") : "");
+        if ((pe->tu.debug || pe->tu.tuneLog) && relaxAlt > 0.0)
+            std::fprintf(stderr, "[shdpe] shard %d tune: relax at 0.8 x delta %.2f ms vs %.2f -> delta %.3f\n",
+                         sh->gindex, relaxAlt, part[rk][0], relaxPick.delta);
     }
     return SHD_PE_OK;
 }
