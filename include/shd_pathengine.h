@@ -175,8 +175,10 @@ int shd_pe_compute_all(ShdPe* pe);
 /* Optional, once, before timed or production use: computes the engine's
  * own rows with each k_batch_rows variant (8 / 6 / 4 waves per SIMD; the
  * relax and post kernels are timed separately and each keeps its faster
- * variant) for later calls (the ranking differs between boxes of the same
- * SKU).  The table is left fully computed; no-op on other paths. */
+ * variant; the chosen relax is also timed at 0.8 x the bucket width and
+ * keeps the faster width -- stats.deltaUsed) for later calls (the ranking
+ * differs between boxes of the same SKU and between shard sizes).  The
+ * table is left fully computed; no-op on other paths. */
 int shd_pe_tune(ShdPe* pe);
 
 /* Compute rows for the given sources (vertex ids, must be attached). */
