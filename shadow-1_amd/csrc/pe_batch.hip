@@ -1183,6 +1183,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             if (!any) break;
         }
         }   // label passes
+        if (dbg && tid == 0) dbg[16 * b + 2] = (int)(((long long)clock64() - ctl->t2) >> 10);   // walks
         // ---- row writer: the lanes' rows are written target block by
         // target block through an LDS tile (the walk stacks' space): a
         // group holds one target of 16 rows, so direct stores would scatter
@@ -1191,46 +1192,85 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // the table is never re-read here)
         if (!failed && !retry) {
             const int T = (int)tab.T;
+            // (2 x NT entries of 21 B: inside the walk stacks' SMAX x NT x 8 B)
             double* const tLat = reinterpret_cast<double*>(smem + BCTRL_BYTES);
-            double* const tRel = tLat + NT;
-            int32_t* const tHop = reinterpret_cast<int32_t*>(tRel + NT);
-            int32_t* const tPred = tHop + NT;
-            uint8_t* const tFlg = reinterpret_cast<uint8_t*>(tPred + NT);
+            double* const tRel = tLat + 2 * NT;
+            int32_t* const tHop = reinterpret_cast<int32_t*>(tRel + 2 * NT);
+            int32_t* const tPred = tHop + 2 * NT;
+            uint8_t* const tFlg = reinterpret_cast<uint8_t*>(tPred + 2 * NT);
             const int wl = tid / NG, wc = tid % NG;     // writer: lane (row), column in block
             const int wrow = laneRow[wl];
             const size_t wbase = (size_t)(wrow >= 0 ? wrow - tab.rowStart : 0) * (size_t)tab.T;
             __syncthreads();                            // walks done: stacks free
-            for (int j0 = 0; j0 < T; j0 += NG) {
-                const int j = j0 + gid;
-                double L = 0.0, Rl = 0.0;
-                int h = -1, pv = -1;
-                uint8_t f = 0;
-                if (row >= 0 && j < T) {
-                    const int t = g.attached[j];
-                    if (t == src) {
-                        // 1-vertex igraph path [s]: the fold uses edge (s,s)
-                        // (:1469-1488); the destination factor is skipped (:1457)
-                        if (g.hasSelf[src]) {
-                            L = 0.0 + g.selfLat[src];
-                            Rl = (1.0 * g.vrel[src]) * g.selfRel[src];
-                            h = 1;
-                        } else {
-                            f |= F_NOEDGE;
-                        }
-                    } else {
-                        const size_t e = (size_t)t * LB + l;
-                        const unsigned long long dt = dec(ld_wg(&D[(size_t)t * LB + l]));
-                        if (dt == INF_BITS) {
+            // WQ targets per group per block, their loads issued branch-free
+            // level by level (vertex id -> dist + label record + vertex
+            // reliability -> parent vertex -> caller id), so WQ dependent
+            // chains are in flight per thread and a block's two barriers are
+            // shared by WQ x NG targets
+            constexpr int WQ = 2;
+            const int BW = WQ * NG;
+            // the lane's own source (1-vertex igraph path [s]: the fold uses
+            // edge (s,s), :1469-1488; the destination factor is skipped, :1457)
+            const bool srcSelf = row >= 0 && g.hasSelf[src >= 0 ? src : 0];
+            const double srcVrel = row >= 0 ? g.vrel[src >= 0 ? src : 0] : 1.0;
+            const double selfL = srcSelf ? 0.0 + g.selfLat[src] : 0.0;
+            const double selfR = srcSelf ? (1.0 * srcVrel) * g.selfRel[src] : 0.0;
+            for (int j0 = 0; j0 < T; j0 += BW) {
+                int tq[WQ], pq[WQ];
+                unsigned long long dq[WQ];
+                Lbl rq[WQ];
+                double vq[WQ];
+#pragma unroll
+                for (int q = 0; q < WQ; ++q) {
+                    const int j = j0 + q * NG + gid;
+                    tq[q] = row >= 0 && j < T ? g.attached[j] : -1;
+                }
+#pragma unroll
+                for (int q = 0; q < WQ; ++q) {
+                    const int tc = tq[q] >= 0 ? tq[q] : 0;
+                    dq[q] = dec(ld_wg(&D[(size_t)tc * LB + l]));
+                    rq[q] = lbl_ld(&LBL[(size_t)tc * LB + l]);
+                    vq[q] = g.vrel[tc];
+                }
+#pragma unroll
+                for (int q = 0; q < WQ; ++q) {
+                    // (an unreachable target's record is not this batch's: its
+                    // arc field is never followed)
+                    const bool reach = tq[q] >= 0 && tq[q] != src && dq[q] != INF_BITS;
+                    const int pa = reach ? rq[q].arc : -1;
+                    const int x = g.inCol[pa >= 0 ? pa & ~TIE_AMB : 0];
+                    pq[q] = pa >= 0 ? x : -1;
+                }
+                if (g.oldId) {
+#pragma unroll
+                    for (int q = 0; q < WQ; ++q) {
+                        const int x = g.oldId[pq[q] >= 0 ? pq[q] : 0];   // device id -> caller's id
+                        pq[q] = pq[q] >= 0 ? x : -1;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < WQ; ++q) {
+                    const int t = tq[q];
+                    double L = 0.0, Rl = 0.0;
+                    int h = -1, pv = -1;
+                    uint8_t f = 0;
+                    if (t >= 0) {
+                        if (t == src) {
+                            if (srcSelf) {
+                                L = selfL;
+                                Rl = selfR;
+                                h = 1;
+                            } else {
+                                f |= F_NOEDGE;
+                            }
+                        } else if (dq[q] == INF_BITS) {
                             f |= F_UNREACHABLE;
                         } else {
-                            L = b2d(dt);
-                            const Lbl er = lbl_ld(&LBL[e]);
-                            h = er.hops;
-                            const int pa = er.arc;
-                            pv = pa >= 0 ? g.inCol[pa & ~TIE_AMB] : -1;
-                            if (pv >= 0 && g.oldId) pv = g.oldId[pv];   // device id -> caller's id
-                            if (g.vrel[src] == 1.0 && g.vrel[t] == 1.0)
-                                Rl = er.rel;
+                            L = b2d(dq[q]);
+                            h = rq[q].hops;
+                            pv = pq[q];
+                            if (srcVrel == 1.0 && vq[q] == 1.0)
+                                Rl = rq[q].rel;
                             else
                                 Rl = fold_rel_batch<LB>(g.vrel, g.inRel, g.inCol, LBL, l, src, t, h);
                             if (L == 0.0) {                 // topology.c:1848-1852
@@ -1239,22 +1279,26 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                             }
                         }
                     }
+                    const int ti = l * BW + q * NG + gid;
+                    tLat[ti] = L;
+                    tRel[ti] = Rl;
+                    tHop[ti] = h;
+                    tPred[ti] = pv;
+                    tFlg[ti] = f;
                 }
-                const int ti = l * NG + gid;
-                tLat[ti] = L;
-                tRel[ti] = Rl;
-                tHop[ti] = h;
-                tPred[ti] = pv;
-                tFlg[ti] = f;
                 __syncthreads();
-                if (wrow >= 0 && j0 + wc < T) {
-                    const int ti2 = wl * NG + wc;
-                    const size_t o = wbase + (size_t)(j0 + wc);
-                    __builtin_nontemporal_store(tLat[ti2], &tab.lat[o]);
-                    __builtin_nontemporal_store(tRel[ti2], &tab.rel[o]);
-                    __builtin_nontemporal_store(tHop[ti2], &tab.hops[o]);
-                    __builtin_nontemporal_store(tFlg[ti2], &tab.flags[o]);
-                    if (tab.pred) __builtin_nontemporal_store(tPred[ti2], &tab.pred[o]);
+#pragma unroll
+                for (int q = 0; q < WQ; ++q) {
+                    const int c = j0 + q * NG + wc;
+                    if (wrow >= 0 && c < T) {
+                        const int ti2 = wl * BW + q * NG + wc;
+                        const size_t o = wbase + (size_t)c;
+                        __builtin_nontemporal_store(tLat[ti2], &tab.lat[o]);
+                        __builtin_nontemporal_store(tRel[ti2], &tab.rel[o]);
+                        __builtin_nontemporal_store(tHop[ti2], &tab.hops[o]);
+                        __builtin_nontemporal_store(tFlg[ti2], &tab.flags[o]);
+                        if (tab.pred) __builtin_nontemporal_store(tPred[ti2], &tab.pred[o]);
+                    }
                 }
                 __syncthreads();
             }
@@ -1352,7 +1396,6 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 atomicAdd(&dbg[16 * b + 10], (int)ctl->dLanes);
             }
             dbg[16 * b + 1] = 0;
-            dbg[16 * b + 2] = 0;
             dbg[16 * b + 3] = (int)needMask;
             dbg[16 * b + 6] = (int)((ctl->t2 - ctl->t1) >> 10);
             dbg[16 * b + 7] = (int)((ctl->t3 - ctl->t2) >> 10);

@@ -952,7 +952,8 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
 // Kernel counters of k_batch_rows (SHD_PE_DEBUG_COUNTERS): phase cycles,
 // re-visits, jump rounds, per-batch cost spread.
 static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t nB) {
-    double ph = 0, pr = 0, kc[5] = {0, 0, 0, 0, 0}, arcsP = 0, lanesP = 0, bmax = 0, bmean = 0, cand = 0;
+    double ph = 0, pr = 0, kc[5] = {0, 0, 0, 0, 0}, arcsP = 0, lanesP = 0, bmax = 0, bmean = 0, cand = 0,
+           walks = 0;
     long ambB = 0, rep = 0;
     double tMin = 1e30, tMax = 0, tSum = 0, tSq = 0;
     for (int32_t i = 0; i < nB; ++i) {
@@ -969,6 +970,7 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
         arcsP += 16.0 * d[9];
         bmax += 1024.0 * d[12]; bmean += 1024.0 * d[13]; cand += d[14];
         lanesP += d[10];
+        walks += 1024.0 * d[2];
     }
     const double mean = tSum / std::max(nB, 1);
     const double sd = std::sqrt(std::max(0.0, tSq / std::max(nB, 1) - mean * mean));
@@ -976,9 +978,10 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
                  sh->gindex, bmax / nB / 1e6, bmean / nB / 1e6, cand / nB);
     std::fprintf(stderr, "[shdpe] batch arc-visits/batch=%.0f (%.2f x nArcs) active lanes/proc=%.2f\n",
                  arcsP / nB, arcsP / nB / (double)pe->hg.nArcs(), lanesP / std::max(pr, 1.0));
-    std::fprintf(stderr, "[shdpe] batch Mcycles/batch: relax=%.2f pred=%.2f labels+write=%.2f tie-export=%.2f tail=%.2f | "
+    std::fprintf(stderr, "[shdpe] batch Mcycles/batch: relax=%.2f pred=%.2f labels+write=%.2f (walks %.2f) tie-export=%.2f tail=%.2f | "
                  "per-batch total min=%.2f mean=%.2f max=%.2f sd=%.2f\n", kc[0] / nB / 1e6, kc[1] / nB / 1e6,
-                 kc[2] / nB / 1e6, kc[3] / nB / 1e6, kc[4] / nB / 1e6, tMin / 1e6, mean / 1e6, tMax / 1e6, sd / 1e6);
+                 kc[2] / nB / 1e6, walks / nB / 1e6, kc[3] / nB / 1e6, kc[4] / nB / 1e6, tMin / 1e6, mean / 1e6,
+                 tMax / 1e6, sd / 1e6);
     std::fprintf(stderr, "[shdpe] batch LB=%d batches=%d grid=%d delta=%.3f | phases/batch=%.1f "
                  "vertex-procs/batch=%.0f (%.2f per vertex) | tie batches=%ld repairs=%ld\n",
                  sh->bcfg.lb, nB, sh->bcfg.grid, sh->bcfg.delta, ph / nB, pr / nB,
