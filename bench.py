@@ -14,7 +14,11 @@ engine-owned RCCL communicator (shd_pe_comm_init + shd_pe_gather: one
 ncclAllGather per field over xGMI) and VERIFIED: the owners' per-row 64-bit
 fingerprints taken before the exchange must equal every rank's fingerprints
 of its assembled table (shdpe/gather.py).  Timed separately, never part of
-`value`, reported under "allgather"; a mismatch exits non-zero.  One-GPU
+`value`, reported under "allgather"; the line is always emitted, and the exit
+status is 0 only for a verified assembly (4 mismatch, 5 RCCL / engine error,
+6 watchdog timeout).  At N > 1 `per_rank` carries every rank's step, kernel
+and exact-kernel time, roofline fraction and rows (min / mean / max and the
+slowest rank), so a scaling line shows where the max-over-ranks time goes.  One-GPU
 rehearsal (BENCH_REHEARSE_ONE_GPU=1, ranks share cuda:0, RCCL refuses such a
 communicator) moves the rows over gloo + shd_pe_put_rows instead.
 
@@ -200,7 +204,7 @@ def main():
                          "process starts the N rank processes itself")
     ap.add_argument("--dry-launch", action="store_true",
                     help="launcher self-test: every rank prints its rank env as JSON and exits")
-    ap.add_argument("--secondary", default="c3a,c3b,c5",
+    ap.add_argument("--secondary", default="c1,c2,c3a,c3b,c5",
                     help="comma list of further configs timed after the headline (rank 0, N=1; "
                          "'' = off): ms_per_step, rows/s and roofline of each")
     ap.add_argument("--host-fill", type=int, default=1,
@@ -312,15 +316,20 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     st = eng.stats()
+    rl = roofline_of(st, n, m_arcs, T, count)
+    per_rank = None
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else f"cuda:{local}")
+        dev = "cpu" if rehearse else f"cuda:{local}"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # every rank's own numbers, so a scaling line shows which rank and
+        # which kernel sets the max-over-ranks time
+        per_rank = collect_per_rank(dist, dev, world, rank_record(st, elapsed, args.steps, count, rl))
         elapsed = float(t.item())
 
     rows_total = T * args.steps
     value = rows_total / elapsed
-    rl = roofline_of(st, n, m_arcs, T, count)
     bound, bytes_per_launch, achieved, avg_launch_ms = (rl["bound"], rl["algorithmic_per_launch"],
                                                         rl["achieved"], rl["avg_launch_ms"])
     traffic = load_traffic(args.workload)
@@ -355,6 +364,8 @@ def main():
         "batch_lanes": st["batchLanes"] or None,
         "batch_post_kernel_waves": st["batchPostWaves"] or None,
     }
+    if per_rank is not None:
+        out["per_rank"] = per_rank
     # ---- N > 1: the shared table assembled on every rank and verified
     # (untimed, never in `value`); a watchdog reports a hung exchange in the
     # line instead of leaving the driver without one ----
@@ -377,7 +388,9 @@ def main():
                                      "error": f"no completion within {args.gather_timeout:.0f} s"})
             sys.stderr.write(f"bench.py: rank {rank}: table assembly timed out\n")
             emit_once(o)
-            os._exit(0)     # value stands; the line says the table was not assembled
+            # the value stands and the line says the table was not assembled;
+            # the exit status says so too (only a verified assembly exits 0)
+            os._exit(EXIT_ASSEMBLY_TIMEOUT)
         wd = threading.Timer(args.gather_timeout, on_timeout)
         wd.daemon = True
         wd.start()
@@ -453,10 +466,68 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    if gather_res is not None and gather_res.get("mismatched_rows_max_over_ranks", 0) > 0:
-        sys.stderr.write(f"bench.py: rank {rank}: assembled table differs from the owners' rows: "
+    rc = assembly_exit_code(gather_res)
+    if rc:
+        sys.stderr.write(f"bench.py: rank {rank}: table assembly not verified (exit {rc}): "
                          f"{json.dumps(gather_res)}\n")
-        sys.exit(4)
+        sys.exit(rc)
+
+
+EXIT_ASSEMBLY_MISMATCH = 4     # assembled rows differ from the owners' fingerprints
+EXIT_ASSEMBLY_ERROR = 5        # RCCL / engine error, or no verdict
+EXIT_ASSEMBLY_TIMEOUT = 6      # the watchdog fired (hung exchange)
+
+
+def assembly_exit_code(gather_res):
+    """0 only for a verified table assembly (or none attempted); the JSON line
+    is emitted first either way, so the measured value is never lost."""
+    if gather_res is None:
+        return 0
+    if gather_res.get("mismatched_rows_max_over_ranks", 0) > 0:
+        return EXIT_ASSEMBLY_MISMATCH
+    if gather_res.get("error") or gather_res.get("verified") is not True:
+        return EXIT_ASSEMBLY_ERROR
+    return 0
+
+
+RANK_FIELDS = ("elapsed_ms_per_step", "kernel_ms_per_step", "exact_ms_per_step", "frac", "rows",
+               "rows_exact")
+
+
+def rank_record(st, elapsed, steps, count, rl):
+    """This rank's numbers for the per-rank block (floats, RANK_FIELDS order)."""
+    k = max(1, steps)
+    kern = st["msSparseKernel"] + st["msDirectKernel"] + st["msDenseKernel"]
+    return [elapsed / k * 1e3, kern / k, st["msExactKernel"] / k, rl["frac"], float(count),
+            float(st["rowsExact"] // k)]
+
+
+def collect_per_rank(dist, dev, world, record):
+    """All-gather every rank's rank_record (one small float64 tensor per rank
+    over the job's process group) and summarise; every rank gets the block."""
+    import torch
+    mine = torch.tensor(record, dtype=torch.float64, device=dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    return per_rank_summary([a.cpu().tolist() for a in allr])
+
+
+def per_rank_summary(records):
+    """N > 1: every rank's step time, kernel time (HIP events on its stream),
+    exact-kernel time, roofline fraction and row count, plus min / mean / max
+    of the step and kernel times and the rank that set the max."""
+    ranks = [dict(zip(RANK_FIELDS, r), rank=i) for i, r in enumerate(records)]
+    for r in ranks:
+        r["rows"] = int(r["rows"])
+        r["rows_exact"] = int(r["rows_exact"])
+    out = {"ranks": ranks}
+    for f in ("elapsed_ms_per_step", "kernel_ms_per_step", "frac"):
+        v = [r[f] for r in ranks]
+        out[f] = {"min": min(v), "mean": sum(v) / len(v), "max": max(v)}
+    out["slowest_rank"] = max(ranks, key=lambda r: r["elapsed_ms_per_step"])["rank"]
+    out["kernel_max_over_mean"] = (out["kernel_ms_per_step"]["max"] /
+                                   max(1e-12, out["kernel_ms_per_step"]["mean"]))
+    return out
 
 
 def secondary(workload, steps, dbg):
@@ -475,7 +546,9 @@ def secondary(workload, steps, dbg):
     eng.compute_all()                        # warm-up
     eng.synchronize()
     eng.reset_stats()
-    k = max(1, min(steps, 3))
+    # small tables (C1: 183 rows, C2) get more steps: their table takes
+    # milliseconds, and one step would be mostly launch overhead noise
+    k = max(1, min(steps, 3 if eng.T > 12_000 else 20))
     t0 = time.perf_counter()
     for _ in range(k):
         eng.compute_all()
@@ -490,6 +563,15 @@ def secondary(workload, steps, dbg):
            "roofline": roofline_of(st, st0["nVertices"], st0["nArcs"], T, T),
            "tie_rows": st["rowsExact"] // k, "ms_exact_per_step": st["msExactKernel"] / k,
            "batch_lanes": st["batchLanes"] or None, "setup_s": setup_s}
+    tr = load_traffic(workload)
+    if tr and tr.get("bytes_per_launch"):
+        # PMC capture of this config's dominant kernel (same kernel sources)
+        rl = out["roofline"]
+        rl["traffic"] = tr["bytes_per_launch"]
+        rl["traffic_tag"] = tr.get("tag")
+        if rl["bound"] == "hbm":
+            rl["traffic_over_algorithmic"] = tr["bytes_per_launch"] / rl["algorithmic_per_launch"]
+            rl["traffic_GBps"] = tr["bytes_per_launch"] / (rl["avg_launch_ms"] * 1e-3) / 1e9
     eng.close()
     return out
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SHD_PE_ABI_VERSION 2
+#define SHD_PE_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------ */
 #define SHD_PE_OK            0
@@ -305,8 +305,15 @@ int shd_pe_synchronize(ShdPe* pe);
 int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbps);
 
 /* Counters of this engine (all its shards).  Both calls take the engine's
- * compute lock: during a running compute they return once it is done. */
+ * compute lock: during a running compute they return once it is done.
+ * ShdPeStats only grows at its end (ABI 3 added rowsTieRepaired): a caller
+ * built against another header than the library's passes its own
+ * sizeof(ShdPeStats) to shd_pe_get_stats_sized, which copies at most that
+ * many bytes (the fields both sides know); shd_pe_stats_size() is the
+ * library's size.  shd_pe_get_stats writes the library's whole struct. */
 int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out);
+int shd_pe_get_stats_sized(const ShdPe* pe, void* out, int64_t outBytes);
+int64_t shd_pe_stats_size(void);
 int shd_pe_reset_stats(ShdPe* pe);
 
 /* ---- batched helpers on the device ------------

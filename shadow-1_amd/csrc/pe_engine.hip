@@ -1433,21 +1433,25 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
             if (perPart ? part[k][1] < part[pk][1] : ms[k] < ms[pk]) pk = k;
         }
         if (!perPart) pk = rk;
-        // bucket width: the chosen relax variant once more at 0.8 x delta,
-        // kept if its relax kernel is faster on this shard (C4 same box: N=1
+        // bucket width: the chosen relax variant at delta and at 0.8 x delta,
+        // timed alternately (A B A B, each width's best run), the narrower
+        // width kept only if its relax kernel is faster by more than 1% on
+        // this shard -- the gain is 1-2% where it exists (C4 same box: N=1
         // -1.2%, the N=8 shard's LB-8 batches -2%; C5 +1.2%, so not a fixed
-        // default; profiles/r05_ab_notes.txt r05bg-bi).  The post kernel does
-        // not use delta.
+        // default; profiles/r05_ab_notes.txt r05bg-bi), and a single run
+        // against a measurement from another pass let noise pick the width.
+        // The post kernel does not use delta.
         BatchLaunch relaxPick = cand[rk];
-        double relaxAlt = 0.0;
+        double relaxAlt = 0.0, relaxBase = 0.0;
         if (perPart) {
             BatchLaunch alt = cand[rk];
             alt.delta = cand[rk].delta * 0.8;
-            sh->bcfg = alt;
             sh->bcfgPost = cand[pk];
-            for (int rep = 0; rep < 2; ++rep) {
+            double best[2] = {0.0, 0.0};
+            for (int rep = 0; rep < 4; ++rep) {
+                sh->bcfg = (rep & 1) ? alt : cand[rk];
                 sh->msPart[0] = sh->msPart[1] = 0.0;
-                sh->timeParts = rep == 1;
+                sh->timeParts = true;
                 const int rc = compute_shard(pe, sh, pos.data(), sh->rowCount);
                 sh->timeParts = false;
                 if (rc) {
@@ -1456,9 +1460,12 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
                     sh->stats = keep;
                     return rc;
                 }
+                double& b = best[rep & 1];
+                if (sh->msPart[0] > 0.0 && (b == 0.0 || sh->msPart[0] < b)) b = sh->msPart[0];
             }
-            relaxAlt = sh->msPart[0];
-            if (relaxAlt > 0.0 && relaxAlt < part[rk][0]) relaxPick = alt;
+            relaxBase = best[0];
+            relaxAlt = best[1];
+            if (relaxAlt > 0.0 && relaxBase > 0.0 && relaxAlt < 0.99 * relaxBase) relaxPick = alt;
             sh->bcfgPost = BatchLaunch{};
         }
         sh->bcfg = relaxPick;
@@ -1475,7 +1482,7 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
                              k == nc - 1 ? (pk == rk ? " -> one variant" : " -> per part") : "");
         if ((pe->tu.debug || pe->tu.tuneLog) && relaxAlt > 0.0)
             std::fprintf(stderr, "[shdpe] shard %d tune: relax at 0.8 x delta %.2f ms vs %.2f -> delta %.3f\n",
-                         sh->gindex, relaxAlt, part[rk][0], relaxPick.delta);
+                         sh->gindex, relaxAlt, relaxBase, relaxPick.delta);
     }
     return SHD_PE_OK;
 }
@@ -2376,6 +2383,17 @@ extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
     t.nShards = (int32_t)pe->shards.size();
     t.msGather = pe->msGather;
     *out = t;
+    return SHD_PE_OK;
+}
+
+extern "C" int64_t shd_pe_stats_size(void) { return (int64_t)sizeof(ShdPeStats); }
+
+extern "C" int shd_pe_get_stats_sized(const ShdPe* pe, void* out, int64_t outBytes) {
+    if (!pe || !out || outBytes <= 0) return SHD_PE_EINVAL;
+    ShdPeStats t;
+    const int rc = shd_pe_get_stats(pe, &t);
+    if (rc) return rc;
+    std::memcpy(out, &t, (size_t)std::min<int64_t>(outBytes, (int64_t)sizeof(ShdPeStats)));
     return SHD_PE_OK;
 }
 

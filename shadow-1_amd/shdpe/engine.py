@@ -28,6 +28,7 @@ EXPORTS = [
     "shd_pe_is_complete", "shd_pe_num_attached", "shd_pe_attached", "shd_pe_compute_all",
     "shd_pe_compute_rows", "shd_pe_compute_positions", "shd_pe_get_row", "shd_pe_get_rows",
     "shd_pe_copy_rows_device", "shd_pe_synchronize", "shd_pe_get_stats", "shd_pe_reset_stats",
+    "shd_pe_get_stats_sized", "shd_pe_stats_size",
     "shd_pe_stream_bandwidth", "shd_pe_num_shards", "shd_pe_shard_bounds", "shd_pe_plan_shards", "shd_pe_owned_range",
     "shd_pe_gather", "shd_pe_comm_unique_id", "shd_pe_comm_init",
     "shd_pe_direct_path", "shd_pe_self_path", "shd_pe_adjacent", "shd_pe_self_paths",
@@ -110,6 +111,8 @@ def load_library(path: str = LIB_PATH):
         "shd_pe_copy_rows_device": (C.c_int, [vp, i32, i32, vp, vp, vp, vp]),
         "shd_pe_synchronize": (C.c_int, [vp]),
         "shd_pe_get_stats": (C.c_int, [vp, vp]),
+        "shd_pe_get_stats_sized": (C.c_int, [vp, vp, C.c_int64]),
+        "shd_pe_stats_size": (C.c_int64, []),
         "shd_pe_reset_stats": (C.c_int, [vp]),
         "shd_pe_stream_bandwidth": (C.c_int, [vp, i64, i32, vp]),
         "shd_pe_num_shards": (i32, [vp]),

@@ -61,3 +61,75 @@ def test_library_stdout_chatter_goes_to_stderr():
     out = [x for x in r.stdout.splitlines() if x.strip()]
     assert len(out) == 2 and all(x.startswith("{") for x in out), r.stdout
     assert "[Gloo]" in r.stderr
+
+
+# ---- N > 1 line shape: per-rank block and the exit status of the assembly ----
+def _import_bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _fake_stats(kernel_ms, exact_ms, rows_exact, steps):
+    return {"msSparseKernel": kernel_ms * steps, "msDirectKernel": 0.0, "msDenseKernel": 0.0,
+            "msExactKernel": exact_ms * steps, "rowsExact": rows_exact * steps}
+
+
+def _per_rank_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    bench = _import_bench()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    steps = 4
+    st = _fake_stats(10.0 + 2 * rank, 0.5 * rank, rank, steps)
+    rl = {"frac": 0.1 + 0.01 * rank}
+    rec = bench.rank_record(st, (11.0 + 2 * rank) * steps * 1e-3, steps, 2048 + rank, rl)
+    q.put((rank, bench.collect_per_rank(dist, "cpu", world, rec)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_per_rank_block_world3_gloo():
+    """What rank 0 puts under `per_rank` at N > 1: every rank's step / kernel
+    / exact time, frac and rows, min / mean / max and the slowest rank --
+    gathered over a real 3-rank gloo group (the GPU runs use RCCL)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() % 500)
+    world = 3
+    procs = [ctx.Process(target=_per_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    blk = got[0]
+    assert all(got[r] == blk for r in range(world))          # every rank holds the same block
+    ranks = blk["ranks"]
+    assert [r["rank"] for r in ranks] == [0, 1, 2]
+    for r in ranks:
+        i = r["rank"]
+        assert abs(r["elapsed_ms_per_step"] - (11.0 + 2 * i)) < 1e-9
+        assert abs(r["kernel_ms_per_step"] - (10.0 + 2 * i)) < 1e-9
+        assert abs(r["exact_ms_per_step"] - 0.5 * i) < 1e-9
+        assert abs(r["frac"] - (0.1 + 0.01 * i)) < 1e-12
+        assert r["rows"] == 2048 + i and r["rows_exact"] == i
+    assert blk["slowest_rank"] == 2
+    assert blk["elapsed_ms_per_step"] == {"min": 11.0, "mean": 13.0, "max": 15.0}
+    assert abs(blk["kernel_max_over_mean"] - 14.0 / 12.0) < 1e-12
+    json.dumps(blk)                                           # it goes into the JSON line
+
+
+def test_assembly_exit_codes():
+    """Only a verified assembly (or none) exits 0; the line is emitted first."""
+    bench = _import_bench()
+    assert bench.assembly_exit_code(None) == 0
+    assert bench.assembly_exit_code({"verified": True, "mismatched_rows_max_over_ranks": 0}) == 0
+    assert bench.assembly_exit_code({"verified": False, "mismatched_rows_max_over_ranks": 3}) == 4
+    assert bench.assembly_exit_code({"verified": False, "error": "RuntimeError: x"}) == 5
+    assert bench.assembly_exit_code({"transport": "rccl"}) == 5        # no verdict
+    assert bench.EXIT_ASSEMBLY_TIMEOUT == 6

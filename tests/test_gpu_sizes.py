@@ -113,6 +113,20 @@ def tie_positions(eng, E):
     return np.array(out, np.int64)
 
 
+def assert_fast_path(st, ctx, ties=False):
+    """The rows came out of the fast kernels, not the safety nets: no tie row
+    failed the exact kernel's slot cross-check (rowsTieRepaired), and no row
+    went to the full igraph-heap emulation -- a tie-free table has no exact
+    rows at all, a sparse tie table only early-stop tie rows (every row that
+    fails the batch kernels' Bellman check goes to the full emulation, so a
+    relax regression shows up here instead of only as a slower bench)."""
+    assert st["rowsTieRepaired"] == 0, f"{ctx}: {st}"
+    if not ties:
+        assert st["rowsExact"] == 0, f"{ctx}: rows left the fast path: {st}"
+    else:
+        assert st["rowsExact"] == st["rowsTieEarly"], f"{ctx}: full-emulation rows: {st}"
+
+
 def whole_table_properties(eng, ctx):
     """Every row: no failures (connected, self-loops), latency > 0,
     reliability in (0, 1], hops >= 1, pred a vertex id off the diagonal
@@ -143,6 +157,7 @@ def test_c2_whole_table(E, oracle_mod, name):
     assert st["rowsComputed"] == att.shape[0] and st["mode"] == 1
     if name == "c2q":
         assert st["rowsExact"] >= 1
+    assert_fast_path(st, name, ties=name == "c2q")
     assert compare_positions(eng, oracle_mod, top, np.arange(eng.T), name, block=1000) == eng.T
     eng.close()
 
@@ -155,6 +170,7 @@ def test_c4_whole_table(E, oracle_mod):
     eng.compute_all()
     st = eng.stats()
     assert st["rowsComputed"] == att.shape[0] and st["mode"] == 1 and st["batched"] == 1
+    assert_fast_path(st, "c4")
     assert compare_positions(eng, oracle_mod, top, np.arange(eng.T), "c4", block=1024) == eng.T
     eng.close()
 
@@ -170,6 +186,7 @@ def test_c4q_tie_rows(E, oracle_mod):
     ties = tie_positions(eng, E)
     assert st["rowsExact"] > 0 and st["rowsTieEarly"] > 0
     assert 0 < ties.shape[0] <= st["rowsExact"]
+    assert_fast_path(st, "c4q", ties=True)
     rng = np.random.default_rng(3)
     pos = np.unique(np.concatenate([ties, rng.choice(eng.T, 256, replace=False)]))
     compare_positions(eng, oracle_mod, top, pos, "c4q", block=256)
@@ -184,6 +201,7 @@ def test_c5_sampled_rows(E, oracle_mod):
     eng.compute_all()
     st = eng.stats()
     assert st["rowsComputed"] == att.shape[0] and st["batched"] == 1
+    assert_fast_path(st, "c5")
     rng = np.random.default_rng(11)
     pos = np.sort(rng.choice(eng.T, 2048, replace=False))
     compare_positions(eng, oracle_mod, top, pos, "c5", block=256)
@@ -200,6 +218,7 @@ def test_c5q_tie_rows(E, oracle_mod):
     st = eng.stats()
     ties = tie_positions(eng, E)
     assert st["rowsExact"] > 0 and ties.shape[0] > 0
+    assert_fast_path(st, "c5q", ties=True)
     rng = np.random.default_rng(5)
     pos = np.unique(np.concatenate([ties, rng.choice(eng.T, 256, replace=False)]))
     compare_positions(eng, oracle_mod, top, pos, "c5q", block=128)
@@ -231,7 +250,9 @@ def test_c3a_complete_whole_table(E):
     eng = E.Engine(top, att)
     assert eng.is_complete
     eng.compute_all()
-    assert eng.stats()["mode"] == 2
+    st = eng.stats()
+    assert st["mode"] == 2
+    assert_fast_path(st, "c3a")
     W, R = _dense_tables(top)
     del top
     n = att.shape[0]
@@ -261,6 +282,7 @@ def test_c3b_dense_minplus(E, oracle_mod):
     eng.compute_all()
     st = eng.stats()
     assert st["mode"] == 3 and st["rowsComputed"] == top.n
+    assert_fast_path(st, "c3b")
     compare_positions(eng, oracle_mod, top, sample, "c3b", block=64)
     np.fill_diagonal(W, np.inf)
     n = top.n
@@ -299,6 +321,7 @@ def test_dense_quantized_tie_rows(E, oracle_mod, quantum):
     eng.compute_all()
     st = eng.stats()
     assert st["mode"] == 3
+    assert st["rowsTieRepaired"] == 0, st          # dense tie rows take the full emulation
     ties = tie_positions(eng, E)
     if quantum >= 1.0:
         assert ties.shape[0] > 0 and st["rowsExact"] >= ties.shape[0]

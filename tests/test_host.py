@@ -44,6 +44,15 @@ def test_library_exports_every_declared_symbol(lib):
     assert sorted(engine.EXPORTS) == syms
 
 
+def test_stats_struct_size_matches_binding(lib):
+    """ShdPeStats grows only at its end: the library reports its size (no GPU
+    call) and the ctypes mirror must match it field for field."""
+    import ctypes
+    from shdpe.engine import Stats
+    assert lib.shd_pe_stats_size() == ctypes.sizeof(Stats)
+    assert Stats._fields_[-1][0] == "rowsTieRepaired"
+
+
 def test_library_is_gfx950_code_object():
     so = os.path.join(ROOT, "shadow-1_amd", "libshdpe.so")
     data = open(so, "rb").read()
