@@ -87,10 +87,23 @@ struct alignas(16) BCtrl {
     // the relax / predecessor phase timestamps (in LDS, not registers: the
     // relax loop runs at its VGPR cap)
     unsigned int dProcs, dArcs, dLanes;
+    unsigned int dWhy;   // SHDPE_DIAG_WHY builds: why the batch's rows left the fast path
     long long t0, t1, t2, t3, t4;
 };
 static_assert(sizeof(BCtrl) <= 128, "batch control block");
 constexpr int BCTRL_BYTES = 128;
+
+// SHDPE_DIAG_WHY (diagnostic builds only, tools/build_variant.sh -D...): per
+// batch, the reasons its rows went to the exact kernel, in dbg[16 b + 1]:
+// 1 failed, 2 Bellman violation in the on-demand predecessor pass, 4 in the
+// full pass, 8 a label walk met an entry without a parent (or the never-spin
+// cap), 16 a walk met an ambiguous entry, 32 deep tree (sweeps), 64 the full
+// pass ran (attempt 1), 128 the relax kernel flagged the batch (phase cap)
+#ifdef SHDPE_DIAG_WHY
+#define DIAG_WHY(bit) (why |= (bit))
+#else
+#define DIAG_WHY(bit) ((void)0)
+#endif
 
 // Entry encoding of the [v][LB] distance array: (f64 bits << 1) | dirty.
 // Positive doubles have bit 63 clear, so the shift loses nothing and the u64
@@ -323,6 +336,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->busySum = 0;
                 ctl->maxOff = 0.0;
                 ctl->dProcs = ctl->dArcs = ctl->dLanes = 0u;
+                ctl->dWhy = 0u;
             }
         }
         fence_wg();
@@ -361,9 +375,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         double bound = delta;
         unsigned long long myFar = INF_BITS;      // smallest far key this thread added
         if constexpr (PT == 2) failed = as_global(bs.flags)[b] != 0;
+#ifdef SHDPE_DIAG_WHY
+        uint32_t why = failed ? 128u : 0u;
+#endif
         uint32_t needMask = 0u;
         for (int attempt = 0;; ++attempt) {
         const bool fullPred = PT != 2 || attempt > 0;
+        if (attempt > 0) DIAG_WHY(64u);
         if (attempt > 0) {
             if (tid == 0) {
                 ctl->qtail = 0;
@@ -1026,6 +1044,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             }
         }
         if (viol) ctl->changed = 1;
+        if (viol) DIAG_WHY(attempt ? 4u : 2u);
         fence_wg();
         __syncthreads();
         const int anyViol = uni(ctl->changed);
@@ -1098,12 +1117,13 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 const int a = xr.arc;
                                 if (a < 0 || ++steps > stepCap) {
                                     if (a >= 0 && pass == 0) deep = true;   // -> sweeps
-                                    else relAmb = 1u;      // no parent / a cycle: exact path
+                                    else { relAmb = 1u; DIAG_WHY(8u); }   // no parent / a cycle: exact path
                                     sp = 0;
                                     found = true;
                                     break;
                                 }
                                 relAmb |= (uint32_t)((a & TIE_AMB) != 0);
+                                if (a & TIE_AMB) DIAG_WHY(16u);
                                 stk[sp * NT + tid] = make_int2(x, a);
                                 ++sp;
                                 const int pe = g.inCol[a & ~TIE_AMB] * LB + l;
@@ -1138,6 +1158,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             }
         }
         if (deep) ctl->changed = 1;
+        if (deep) DIAG_WHY(32u);
         fence_wg();
         __syncthreads();
         const int anyDeep = uni(ctl->changed);
@@ -1380,6 +1401,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             tieSlot[tid] = -1;
         }
         __syncthreads();
+#ifdef SHDPE_DIAG_WHY
+        if (failed) why |= 1u;
+        if (why) atomicOr(&ctl->dWhy, why);
+        __syncthreads();
+#endif
         if (dbg && tid == 0) ctl->t4 = (long long)clock64();
         // 0 fast path, 1 full igraph-heap emulation, 2 + slot: early-stop
         // emulation with the exported tie data
@@ -1395,7 +1421,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 atomicAdd(&dbg[16 * b + 9], (int)(ctl->dArcs >> 4));
                 atomicAdd(&dbg[16 * b + 10], (int)ctl->dLanes);
             }
-            dbg[16 * b + 1] = 0;
+            dbg[16 * b + 1] = (int)ctl->dWhy;
             dbg[16 * b + 3] = (int)needMask;
             dbg[16 * b + 6] = (int)((ctl->t2 - ctl->t1) >> 10);
             dbg[16 * b + 7] = (int)((ctl->t3 - ctl->t2) >> 10);

@@ -360,7 +360,8 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
     (void)hipMemsetAsync(rowAmb, 0, nRows, st);
     const unsigned gx = (unsigned)((n + TCOL - 1) / TCOL);
     const dim3 gridS((unsigned)((nRows + 16 * MI_SWEEP - 1) / (16 * MI_SWEEP)), gx);
-    const int miP = tu.densePredMi == 4 || tu.densePredMi == 6 ? tu.densePredMi : MI_PRED;
+    const int miP = tu.densePredMi >= 3 && tu.densePredMi <= 6 && tu.densePredMi != 5 ? tu.densePredMi
+                                                                                         : MI_PRED;
     const dim3 gridP((unsigned)((nRows + 16 * miP - 1) / (16 * miP)), gx);
     // chunk epochs (uint8): sweep t visits chunks changed at t-1 or t; the
     // initial rows count as changed at epoch 0.  Off beyond 250 sweeps or
@@ -398,6 +399,9 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
     }
     if (miP == 6)
         hipLaunchKernelGGL((k_minplus<MP_PRED, 6>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
+                           rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
+    else if (miP == 3)
+        hipLaunchKernelGGL((k_minplus<MP_PRED, 3>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
                            rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
     else if (miP == 4)
         hipLaunchKernelGGL((k_minplus<MP_PRED, 4>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,

@@ -982,6 +982,16 @@ static void print_batch_debug(ShdPe* pe, Shard* sh, const int32_t* d0, int32_t n
                  "per-batch total min=%.2f mean=%.2f max=%.2f sd=%.2f\n", kc[0] / nB / 1e6, kc[1] / nB / 1e6,
                  kc[2] / nB / 1e6, walks / nB / 1e6, kc[3] / nB / 1e6, kc[4] / nB / 1e6, tMin / 1e6, mean / 1e6,
                  tMax / 1e6, sd / 1e6);
+    // SHDPE_DIAG_WHY builds: per reason bit, the batches it fired in
+    long why[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool anyWhy = false;
+    for (int32_t i = 0; i < nB; ++i)
+        for (int k = 0; k < 8; ++k)
+            if ((d0[16 * i + 1] >> k) & 1) { ++why[k]; anyWhy = true; }
+    if (anyWhy)
+        std::fprintf(stderr, "[shdpe] batch why: failed=%ld viol-ondemand=%ld viol-full=%ld noparent=%ld "
+                     "ambiguous=%ld deep=%ld fullpass=%ld relax-flag=%ld\n", why[0], why[1], why[2],
+                     why[3], why[4], why[5], why[6], why[7]);
     std::fprintf(stderr, "[shdpe] batch LB=%d batches=%d grid=%d delta=%.3f | phases/batch=%.1f "
                  "vertex-procs/batch=%.0f (%.2f per vertex) | tie batches=%ld repairs=%ld\n",
                  sh->bcfg.lb, nB, sh->bcfg.grid, sh->bcfg.delta, ph / nB, pr / nB,
