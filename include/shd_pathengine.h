@@ -143,6 +143,11 @@ typedef struct ShdPeStats {
     int64_t rowsTieRepaired;   /* early-stop tie rows whose exported slot failed the
                                   exact kernel's distance cross-check and were
                                   recomputed by the full emulation (0 when correct) */
+    int32_t batchCoop;         /* relax kernel in use: workgroups per batch (>= 2:
+                                  the cooperative relax of small shards; 0 plain) */
+    int64_t relaxCoopAborts;   /* cooperative relax launches refused or aborted (a
+                                  barrier wait ran too long); each round was
+                                  recomputed by the plain relax */
 } ShdPeStats;
 
 /* Defaults for ShdPeOptions. */
@@ -306,7 +311,8 @@ int shd_pe_stream_bandwidth(ShdPe* pe, int64_t bytes, int32_t iters, double* gbp
 
 /* Counters of this engine (all its shards).  Both calls take the engine's
  * compute lock: during a running compute they return once it is done.
- * ShdPeStats only grows at its end (ABI 3 added rowsTieRepaired): a caller
+ * ShdPeStats only grows at its end (ABI 3 added rowsTieRepaired, batchCoop,
+ * relaxCoopAborts): a caller
  * built against another header than the library's passes its own
  * sizeof(ShdPeStats) to shd_pe_get_stats_sized, which copies at most that
  * many bytes (the fields both sides know); shd_pe_stats_size() is the

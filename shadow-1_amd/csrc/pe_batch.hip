@@ -89,6 +89,7 @@ struct alignas(16) BCtrl {
     unsigned int dProcs, dArcs, dLanes;
     unsigned int dWhy;   // SHDPE_DIAG_WHY builds: why the batch's rows left the fast path
     long long t0, t1, t2, t3, t4;
+    int pubCnt;          // cooperative relax: near bits this member published this phase
 };
 static_assert(sizeof(BCtrl) <= 128, "batch control block");
 constexpr int BCTRL_BYTES = 128;
@@ -121,17 +122,107 @@ constexpr unsigned long long INF_ENC = INF_BITS << 1;   // +inf, clean
 // (perturbation variants of these three -- plain stores, doubled atomics,
 // doubled reads -- are patches under tools/variants/, built by
 // tools/build_variant.sh for same-box A/B runs)
+// CO = the cooperative relax (PART 3): several workgroups of one XCD share
+// the batch's dist array, so its loads are agent scope (past this CU's L1,
+// served by the XCD's L2, where a partner's plain stores land and from which
+// its memory-side atomics evict the line).  A stale L1 copy would be harmful
+// only in one way -- a vertex listed from a partner's near bit, read clean
+// or with an older dirty value, relaxed (or skipped) and marked clean while
+// the partner's newer value, whose near bit was just consumed, is never
+// relaxed -- but it must not happen at all.
+template <bool CO = false>
+__device__ __forceinline__ unsigned long long ld_d(unsigned long long* p) {
+    if constexpr (CO)
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        return ld_wg(p);
+}
+
+template <bool CO = false>
 __device__ __forceinline__ void relax_min(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, CO ? __HIP_MEMORY_SCOPE_AGENT : __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // relax pre-check load
+template <bool CO = false>
 __device__ __forceinline__ unsigned long long relax_ld(unsigned long long* D, int x, int LB, int l) {
-    return ld_wg(&D[(size_t)x * LB + l]);
+    return ld_d<CO>(&D[(size_t)x * LB + l]);
 }
 
+template <bool CO = false>
 __device__ __forceinline__ void mark_clean(unsigned long long* p, unsigned long long e) {
-    __hip_atomic_fetch_min(p, e & ~1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_min(p, e & ~1ull, __ATOMIC_RELAXED, CO ? __HIP_MEMORY_SCOPE_AGENT : __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ---- cooperative relax: group formation and the group barrier ----------
+// A launch of PART 3 is cooperative (hipLaunchCooperativeKernel: every
+// workgroup resident).  Each workgroup registers on its XCD (HW_REG_XCC_ID)
+// and waits until all have; the workgroups of one XCD then form groups of K
+// (the last one of an XCD may be smaller), so a group's members always share
+// the XCD's L2 -- whatever the dispatcher's placement.  Every poll loop
+// gives up after bs.coSpin polls and sets the launch's abort word; every
+// workgroup that sees it returns at once, and the host recomputes the round
+// with the plain relax (never a wrong or a missing row).
+__device__ __forceinline__ int co_ld(int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void co_abort(const BatchScratch& bs) {
+    __hip_atomic_store(&bs.coCtl[17], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// lane 0 of a workgroup: out = {group, member, group size, groups}; 0 = abort
+__device__ int co_register(const BatchScratch& bs, int* out) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    x &= 15u;
+    const int K = bs.coK;
+    const int r = __hip_atomic_fetch_add(&bs.coCtl[x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&bs.coCtl[16], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int spin = 0; co_ld(&bs.coCtl[16]) < (int)gridDim.x; ++spin) {
+        if (spin > bs.coSpin || co_ld(&bs.coCtl[17])) {
+            co_abort(bs);
+            return 0;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    int base = 0, total = 0;
+    for (int y = 0; y < 16; ++y) {
+        const int ng = (co_ld(&bs.coCtl[y]) + K - 1) / K;
+        base += y < (int)x ? ng : 0;
+        total += ng;
+    }
+    const int c = co_ld(&bs.coCtl[x]);
+    out[0] = base + r / K;
+    out[1] = r % K;
+    out[2] = min(K, c - (r / K) * K);
+    out[3] = total;
+    return 1;
+}
+
+// group barrier: every wave's memory operations complete, one arrival per
+// member on the group's counter, a poll until all K arrived for this epoch;
+// false = abort (the poll ran too long, or another workgroup aborted)
+__device__ __forceinline__ bool co_barrier(const BatchScratch& bs, int* bar, int K, int& epoch, int* sOk) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    ++epoch;
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int target = epoch * K;
+        int ok = 1;
+        for (int spin = 0; co_ld(bar) < target; ++spin) {
+            if (spin > bs.coSpin || co_ld(&bs.coCtl[17])) {
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (ok && co_ld(&bs.coCtl[17])) ok = 0;
+        if (!ok) co_abort(bs);
+        *sOk = ok;
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(*sOk) != 0;
 }
 
 // Pending bitmaps (one bit per vertex, near + far sets): in LDS when both
@@ -267,7 +358,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                                            int32_t nBatches, uint8_t* rowAmbig,
                                                            double delta, int32_t* dbg,
                                                            const TieBuf* __restrict__ tieDesc) {
-    constexpr int PT = PART;
+    // PART 3: the relax (PART 1) shared by K workgroups per batch -- its own
+    // instantiation, so the plain relax keeps its code and register budget
+    constexpr bool CO = PART == 3;
+    constexpr int PT = CO ? 1 : PART;
     constexpr int BV = BCfg<WPE>::BV;
     constexpr int SMAX = BCfg<WPE>::SMAX;
     // the light-vertex relax loop and the predecessor pass are software-
@@ -304,11 +398,27 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     BLabel* LBL = as_global(bs.L + slot * SE);
     int32_t* Q = as_global(bs.queue + slot * NS);
 
+    // cooperative relax: this workgroup's group (same XCD), member index and
+    // group size; batches are assigned statically, group by group
+    int coGroup = 0, coMember = 0, coK = 1, coNG = 1, coEpoch = 0, coPP = 0, coIter = 0;
+    int* coBar = nullptr;
+    __shared__ int sCo[5];
+    if constexpr (CO) {
+        if (tid == 0) sCo[4] = co_register(bs, sCo);
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(sCo[4])) return;        // abort: the host reruns the round
+        coGroup = __builtin_amdgcn_readfirstlane(sCo[0]);
+        coMember = __builtin_amdgcn_readfirstlane(sCo[1]);
+        coK = __builtin_amdgcn_readfirstlane(sCo[2]);
+        coNG = __builtin_amdgcn_readfirstlane(sCo[3]);
+        coBar = as_global(bs.coBars) + (size_t)coGroup * 32;
+    }
+
     // batches are taken from a device counter (dynamic: a batch's cost varies
     // by ~20%, and a workgroup finishing early takes the next one)
     __shared__ int nextB;
     for (;;) {
-        if (tid == 0) nextB = atomicAdd(bs.next, 1);
+        if (tid == 0) nextB = CO ? coGroup + (coIter++) * coNG : atomicAdd(bs.next, 1);
         __syncthreads();
         const int b = nextB;
         if (b >= nBatches) break;
@@ -321,8 +431,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             ulonglong2* D2 = reinterpret_cast<ulonglong2*>(D);
             const size_t cnt2 = NE / 2;
             const ulonglong2 inf2 = make_ulonglong2(INF_ENC, INF_ENC);
-            if constexpr (PT != 2)
-                for (size_t i = tid; i < cnt2; i += NT) D2[i] = inf2;
+            if constexpr (PT != 2) {
+                // (cooperative: each member its slice of the shared array)
+                const size_t i0 = cnt2 * coMember / coK, i1 = cnt2 * (coMember + 1) / coK;
+                for (size_t i = i0 + tid; i < i1; i += NT) D2[i] = inf2;
+            }
             for (int w = tid; w < nwp; w += NT) { any0.st(w, 0u); any1.st(w, 0u); }
             if (tid == 0) {
                 ctl->qtail = 0;
@@ -337,15 +450,18 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->maxOff = 0.0;
                 ctl->dProcs = ctl->dArcs = ctl->dLanes = 0u;
                 ctl->dWhy = 0u;
+                ctl->pubCnt = 0;
             }
         }
         fence_wg();
         __syncthreads();
+        if constexpr (CO)      // every member's slice is +inf before any source entry
+            if (!co_barrier(bs, coBar, coK, coEpoch, &sCo[4])) return;
         // lane offset: the source's distance to its nearest hub (host plan);
         // key = dist + (maxOff - off) lines the lanes up behind the hub
         const double off = (row >= 0 && bs.rowOff) ? as_global(bs.rowOff)[row] : 0.0;
         if (gid == 0) atomicMax(reinterpret_cast<unsigned long long*>(&ctl->maxOff), d2b(off));
-        if (PT != 2 && gid == 0 && src >= 0) {
+        if (PT != 2 && gid == 0 && src >= 0 && coMember == 0) {
             D[(size_t)src * LB + l] = enc_dirty(d2b(0.0));
             any0.set(src);
         }
@@ -397,14 +513,75 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             if (failed) break;
             const Bits<GB> anyC = par ? any1 : any0;   // near
             const Bits<GB> anyF = par ? any0 : any1;   // far
+            // cooperative relax: each member publishes its near bits (set by
+            // its own relaxations) and its far state, and after the group
+            // barrier lists the group's union of near bits for the words it
+            // owns (w = member mod K); the bucket advance and the end follow
+            // the group's totals, so every member takes the same decisions
+            uint32_t* coPn = nullptr;
+            int coNear = 0, coFar = 0;
+            unsigned long long coFmin = INF_BITS;
+            if constexpr (CO) {
+                if (myFar != INF_BITS) {
+                    atomicMin(&ctl->farMin, myFar);
+                    myFar = INF_BITS;
+                }
+                coPP ^= 1;      // two buffers: a member publishing phase p + 1 never
+                                // overwrites what a partner still reads of phase p
+                coPn = as_global(bs.coPub) + ((size_t)coGroup * 2 + coPP) * (size_t)bs.coK * nwp;
+                unsigned long long* const ps =
+                    as_global(bs.coPubS) + ((size_t)coGroup * 2 + coPP) * (size_t)bs.coK * 2;
+                int cnt = 0;
+                for (int w = tid; w < nw; w += NT) {
+                    const uint32_t bits = anyC.ld(w);
+                    __hip_atomic_store(&coPn[(size_t)coMember * nwp + w], bits, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    if (bits) {
+                        anyC.st(w, 0u);
+                        cnt += __popc(bits);
+                    }
+                }
+                if (cnt) atomicAdd(&ctl->pubCnt, cnt);
+                fence_wg();
+                __syncthreads();
+                if (tid == 0) {
+                    __hip_atomic_store(&ps[coMember * 2],
+                                       (unsigned long long)(unsigned)ctl->pubCnt |
+                                           ((unsigned long long)(ctl->farAny != 0) << 32),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&ps[coMember * 2 + 1], ctl->farMin, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    ctl->pubCnt = 0;
+                }
+                if (!co_barrier(bs, coBar, coK, coEpoch, &sCo[4])) return;
+                for (int k = 0; k < coK; ++k) {
+                    const unsigned long long a =
+                        __hip_atomic_load(&ps[k * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long f =
+                        __hip_atomic_load(&ps[k * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    coNear |= (a & 0xFFFFFFFFull) != 0;
+                    coFar |= (int)(a >> 32);
+                    coFmin = f < coFmin ? f : coFmin;
+                }
+                coNear = uni(coNear);
+                coFar = uni(coFar);
+                coFmin = d2b(uni(b2d(coFmin)));
+            }
             // candidates = vertices with a near bit (consumed)
             // (hubs -- degree >= the engine's heavy threshold -- go to a list
             // of their own, processed by whole waves: one 16-lane group on a
             // hub's ~1000 arcs would set the phase's length)
-            for (int w = tid; w < nw; w += NT) {
-                uint32_t bits = anyC.ld(w);
+            for (int w = CO ? coMember + tid * coK : tid; w < nw; w += CO ? NT * coK : NT) {
+                uint32_t bits = 0u;
+                if constexpr (CO) {
+                    for (int k = 0; k < coK; ++k)
+                        bits |= __hip_atomic_load(&coPn[(size_t)k * nwp + w], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    bits = anyC.ld(w);
+                }
                 if (bits) {
-                    anyC.st(w, 0u);
+                    if constexpr (!CO) anyC.st(w, 0u);
                     uint32_t hv = bits & g.heavyBits[w];
                     bits &= ~hv;
                     if (bits) {
@@ -433,10 +610,10 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             __syncthreads();
             const int qn = uni(ctl->qtail);
             const int hn = uni(ctl->htail);
-            if (qn == 0 && hn == 0) {
+            if (CO ? !coNear : qn == 0 && hn == 0) {
                 // bucket settled: advance to the far set, or done
-                const int farAny = uni(ctl->farAny);
-                const double fm = uni(b2d(ctl->farMin));
+                const int farAny = CO ? coFar : uni(ctl->farAny);
+                const double fm = CO ? b2d(coFmin) : uni(b2d(ctl->farMin));
                 __syncthreads();
                 if (!farAny) break;
                 bound = uni(fm < b2d(INF_BITS) ? next_bound(fm, delta) : b2d(INF_BITS));
@@ -463,7 +640,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 for (int h = wv; h < hn; h += NW) {
                     const int u = ld_wg(&Q[NS - 1 - h]);
                     unsigned long long* const pu = &D[(size_t)u * LB + l];
-                    const unsigned long long e0 = ld_wg(pu);
+                    const unsigned long long e0 = ld_d<CO>(pu);
                     const int a0 = g.rowPtr[u], a1 = g.rowPtr[u + 1];
                     const double k0 = b2d(dec(e0)) + sh;
                     const bool dirty = is_dirty(e0);
@@ -477,7 +654,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
                         farAdd = 1;
                     }
-                    if (gw == 0 && act) mark_clean(pu, e0);
+                    if (gw == 0 && act) mark_clean<CO>(pu, e0);
                     const unsigned long long dub1 = act ? dec(e0) : INF_BITS;
                     if (!__ballot(amask != 0)) continue;       // wave-uniform
                     if (dbg && gw == 0 && l == 0) {
@@ -499,7 +676,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         }
 #pragma unroll
                         for (int k = 0; k < BK; ++k)
-                            dx[k] = relax_ld(D, xs[k] >= 0 ? xs[k] : 0, LB, l);
+                            dx[k] = relax_ld<CO>(D, xs[k] >= 0 ? xs[k] : 0, LB, l);
 #pragma unroll
                         for (int k = 0; k < BK; ++k) {
                             const int x = xs[k];
@@ -508,7 +685,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                 const double nd = b2d(dub1) + ws[k];
                                 const unsigned long long nb = d2b(nd);
                                 if (nb < dec(dx[k])) {
-                                    relax_min(&D[(size_t)x * LB + l], enc_dirty(nb));
+                                    relax_min<CO>(&D[(size_t)x * LB + l], enc_dirty(nb));
                                     const double kx = nd + sh;
                                     impN = kx < bound;
                                     impF = !impN;
@@ -554,7 +731,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             auto q_at = [&](int i) { return i < qn ? ld_wg(&Q[min(i, qc)]) : -1; };
             auto ld_head = [&](int uu, unsigned long long& d, int& r0, int& r1) {
                 const int uc = uu >= 0 ? uu : 0;
-                const unsigned long long d0 = ld_wg(&D[(size_t)uc * LB + l]);
+                const unsigned long long d0 = ld_d<CO>(&D[(size_t)uc * LB + l]);
                 const int x0 = g.rowPtr[uc], x1 = g.rowPtr[uc + 1];
                 d = uu >= 0 ? d0 : INF_ENC;
                 r0 = uu >= 0 ? x0 : 0;
@@ -614,7 +791,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         myFar = d2b(k0) < myFar ? d2b(k0) : myFar;
                         farAdd = 1;
                     }
-                    if (act) mark_clean(&D[(size_t)uC[v] * LB + l], dbC[v]);
+                    if (act) mark_clean<CO>(&D[(size_t)uC[v] * LB + l], dbC[v]);
                     dub[v] = act ? dec(dbC[v]) : INF_BITS;
                     deg[v] = amask ? a1C[v] - a0C[v] : 0;          // group-uniform
                     if (amask && dbg && l == 0) {
@@ -652,7 +829,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
                             for (int k = 0; k < BKR; ++k)
-                                dx[v][k] = relax_ld(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l);
+                                dx[v][k] = relax_ld<CO>(D, xs[v][k] >= 0 ? xs[v][k] : 0, LB, l);
 #pragma unroll
                         for (int v = 0; v < BV; ++v)
 #pragma unroll
@@ -663,7 +840,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                                     const double nd = b2d(dub[v]) + ws[v][k];
                                     const unsigned long long nb = d2b(nd);
                                     if (nb < dec(dx[v][k])) {
-                                        relax_min(&D[(size_t)x * LB + l], enc_dirty(nb));
+                                        relax_min<CO>(&D[(size_t)x * LB + l], enc_dirty(nb));
                                         const double kx = nd + sh;
                                         impN = kx < bound;
                                         impF = !impN;
@@ -702,9 +879,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 ctl->qhead = 0;
                 ctl->htail = 0;
                 if (dbg) {
-                    dbg[16 * b + 12] += (int)(ctl->busyMax >> 10);
-                    dbg[16 * b + 13] += (int)((ctl->busySum / NG) >> 10);
-                    dbg[16 * b + 14] += qn;
+                    atomicAdd(&dbg[16 * b + 12], (int)(ctl->busyMax >> 10));
+                    atomicAdd(&dbg[16 * b + 13], (int)((ctl->busySum / NG) >> 10));
+                    atomicAdd(&dbg[16 * b + 14], qn);
                     ctl->busyMax = 0;
                     ctl->busySum = 0;
                 }
@@ -1062,7 +1239,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         ++repairs;
         }   // verification loop
         if constexpr (PT == 1) {
-            if (tid == 0) as_global(bs.flags)[b] = failed ? 1 : 0;
+            if (tid == 0 && coMember == 0) as_global(bs.flags)[b] = failed ? 1 : 0;
             break;
         }
         if (dbg && tid == 0) ctl->t2 = (long long)clock64();
@@ -1085,7 +1262,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         // deep trees (a walk over WALK_BUDGET steps: restarts cost
         // O(depth^2 / SMAX)) switch to Gauss-Seidel sweeps over all entries
         // and a second writer pass.
-        uint32_t relAmb = 0u;
+        // latency floor: the lane's own source must sit at distance exactly 0
+        // in the array its row is written from (latencies are > 0, so only
+        // the source is) -- an array that is not this lane's sends the row to
+        // the exact kernel, never to the table
+        uint32_t relAmb = row >= 0 && dec(ld_wg(&D[(size_t)(src >= 0 ? src : 0) * LB + l])) != 0ull ? 1u : 0u;
         bool retry = false;
         for (int pass = 0; pass < 2; ++pass) {
         bool deep = false;
@@ -1340,9 +1521,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if constexpr (PT == 1) {
             __syncthreads();
             if (dbg && tid == 0) {
-                dbg[16 * b + 0] = phases;
-                dbg[16 * b + 5] = (int)((ctl->t1 - ctl->t0) >> 10);
-                dbg[16 * b + 15] = repairs;
+                if (coMember == 0) {
+                    dbg[16 * b + 0] = phases;
+                    dbg[16 * b + 5] = (int)((ctl->t1 - ctl->t0) >> 10);
+                    dbg[16 * b + 15] = repairs;
+                }
                 atomicAdd(&dbg[16 * b + 4], (int)ctl->dProcs);
                 atomicAdd(&dbg[16 * b + 9], (int)(ctl->dArcs >> 4));
                 atomicAdd(&dbg[16 * b + 10], (int)ctl->dLanes);
@@ -1442,6 +1625,65 @@ static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
     hipLaunchKernelGGL((k_batch_rows<LB, WPE, GB, PART>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g,
                        tab, bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
+}
+
+// The cooperative relax (PART 3) exists for LB 8 and 16 with LDS bitmaps --
+// the small-shard configurations it is for.  Launched cooperatively: the
+// runtime refuses a grid that is not wholly resident (then the caller runs
+// the plain relax).
+template <int LB, int WPE>
+static int launch_coop_lb(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
+                          const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
+                          const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st,
+                          int grid) {
+    const void* fn = reinterpret_cast<const void*>(&k_batch_rows<LB, WPE, false, 3>);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
+    DevGraph a0 = g;
+    DevTable a1 = tab;
+    BatchScratch a2 = bs;
+    const int32_t* a3 = dBatchRows;
+    int32_t a4 = nBatches;
+    uint8_t* a5 = dRowAmbig;
+    double a6 = cfg.delta;
+    int32_t* a7 = dDbg;
+    const TieBuf* a8 = tie;
+    void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
+    return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(cfg.threads), args, (unsigned)cfg.ldsBytes, st) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+
+template <int WPE>
+static int launch_coop_w(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
+                         const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
+                         const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, hipStream_t st, int grid) {
+    if (cfg.lb == 8)
+        return launch_coop_lb<8, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+    return launch_coop_lb<16, WPE>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, grid);
+}
+
+int launch_batch_relax_coop(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
+                            const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
+                            const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream) {
+    if (nBatches <= 0) return 0;
+    if (cfg.gbits || (cfg.lb != 8 && cfg.lb != 16) || cfg.grid <= 0) return -1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (cfg.wpe >= 8)
+        return launch_coop_w<8>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, cfg.grid);
+    if (cfg.wpe == 6)
+        return launch_coop_w<6>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, cfg.grid);
+    return launch_coop_w<4>(g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg, dDbg, tie, st, cfg.grid);
+}
+
+const void* batch_coop_kernel_ptr(int lb, int wpe) {
+    if (lb == 8)
+        return wpe >= 8 ? reinterpret_cast<const void*>(&k_batch_rows<8, 8, false, 3>)
+             : wpe == 6 ? reinterpret_cast<const void*>(&k_batch_rows<8, 6, false, 3>)
+                        : reinterpret_cast<const void*>(&k_batch_rows<8, 4, false, 3>);
+    return wpe >= 8 ? reinterpret_cast<const void*>(&k_batch_rows<16, 8, false, 3>)
+         : wpe == 6 ? reinterpret_cast<const void*>(&k_batch_rows<16, 6, false, 3>)
+                    : reinterpret_cast<const void*>(&k_batch_rows<16, 4, false, 3>);
 }
 
 int batch_threads(int wpe) { return wpe == 6 ? 768 : BT_THREADS; }

@@ -93,6 +93,11 @@ struct Tuning {
     int tuneLog = 0;           // print shd_pe_tune's per-variant times (no kernel counters)
     int tieCorrupt = 0;        // tests only: scale one early-stop slot's exported distances
                                // after the relevance scan (exercises the tie-slot repair)
+    int batchCoop = 0;         // cooperative relax: K workgroups per batch (>= 2 forces it,
+                               // 0 = the tune decides, -1 = never)
+    int batchCoopWpe = 0;      // its variant (8 / 6 / 4 waves; 0 = the one with two
+                               // workgroups per CU)
+    int coopSpin = 1 << 22;    // its barrier poll limit (tests shrink it to force aborts)
 };
 
 struct DevScratch {
@@ -132,6 +137,16 @@ struct BatchScratch {
     int32_t* flags;          // split kernels: per batch of the round, 1 = phase cap hit
     const double* rowOff;    // [T] per table position: the source's distance to its
                              // batch hub (bucket key offset; null = no offsets)
+    // cooperative relax (PART 3 of k_batch_rows): K workgroups of one XCD
+    // share a batch; the group state below is zeroed by the host before
+    // every launch
+    int32_t* coCtl;          // [0..15] workgroups registered per XCD, [16] registered,
+                             // [17] abort (a barrier wait ran past coSpin polls)
+    int32_t* coBars;         // [group * 32]: one barrier counter per group (own line)
+    uint32_t* coPub;         // [group][2][K][nwp] published near bits (two buffers)
+    unsigned long long* coPubS;   // [group][2][K][2] published near count | far flag, far min
+    int32_t coK;             // members per group (PART 3 only)
+    int32_t coSpin;          // barrier poll limit (s_sleep 1 each)
 };
 
 struct BatchLaunch {
@@ -143,6 +158,8 @@ struct BatchLaunch {
     double delta;            // bucket width
     int32_t gbits;           // 1: pending bitmaps in global scratch (n > ~655k vertices)
     int32_t split;           // 1: relax and post as two kernels over rounds of batches
+    int32_t coop;            // relax: K >= 2 workgroups (one XCD) per batch, PART 3 kernel
+                             // launched cooperatively (all resident); 0 / 1: off
 };
 
 // Tie export (pe_batch.hip -> k_exact_rows early stop -> k_tie_write): per
@@ -231,6 +248,12 @@ void launch_batch_rows(const DevGraph& g, const DevTable& tab, const BatchScratc
                        const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* dTie, void* stream,
                        int part = 0);
 const void* batch_kernel_ptr(int lb, int wpe, bool gbits, int part = 0);
+// cooperative relax (PART 3; LB 8 / 16, LDS bitmaps): 0 launched, -1 refused
+// (grid not resident / unsupported shape: run launch_batch_rows part 1)
+int launch_batch_relax_coop(const DevGraph& g, const DevTable& tab, const BatchScratch& bs,
+                            const int32_t* dBatchRows, int32_t nBatches, uint8_t* dRowAmbig,
+                            const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream);
+const void* batch_coop_kernel_ptr(int lb, int wpe);
 int batch_lds_bytes(int n, int wpe, bool gbits);
 int batch_threads(int wpe);    // workgroup size of a variant (6 waves: 768, else 1024)
 int64_t batch_bits_words(int n);   // per slot, both bitmaps

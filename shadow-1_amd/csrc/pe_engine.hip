@@ -72,6 +72,9 @@ struct Shard {
     BatchLaunch bcfgAlt2{};         // a third variant (6 waves), shd_pe_tune
     BatchLaunch bcfgPost{};         // split kernels: post-kernel variant when the tune picked
                                     // another one than bcfg's (grid 0: bcfg)
+    BatchLaunch bcfgCoop{};         // cooperative relax candidate (coop >= 2; grid 0: none)
+    int64_t coopAborts = 0;         // cooperative relax launches aborted (round rerun plain)
+    int32_t* dCoopAbort = nullptr;  // host-mapped copy target of the abort word
     bool tuned = false;
     bool timeParts = false;         // split kernels: time relax / post launches (tune)
     double msPart[2] = {0.0, 0.0};
@@ -183,6 +186,9 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_STREAM_WG_PER_CU", t.streamWgPerCU);
     gi("SHDPE_TIE_CORRUPT", t.tieCorrupt);
     gi("SHDPE_TUNE_LOG", t.tuneLog);
+    gi("SHDPE_BATCH_COOP", t.batchCoop);
+    gi("SHDPE_BATCH_COOP_WPE", t.batchCoopWpe);
+    gi("SHDPE_COOP_SPIN", t.coopSpin);
 }
 
 extern "C" void shd_pe_default_options(ShdPeOptions* opt) {
@@ -356,6 +362,36 @@ static int configure(ShdPe* pe, Shard* sh) {
     sh->bcfg = b;
     sh->bcfgPost = BatchLaunch{};
     if (!forced && first == 4 && ok6 && b.split && b.lb >= 16) sh->bcfgPost = v6.first;
+    // Cooperative relax (PART 3, K workgroups of one XCD per batch): for a
+    // shard with fewer batches than the plain relax has workgroup slots --
+    // the C4 8-GPU shard's 256 LB-8 batches leave one of the two 8-wave
+    // slots of every CU idle -- the batch's listing rounds are shared by K
+    // workgroups.  A candidate of shd_pe_tune; SHDPE_BATCH_COOP=K forces it.
+    sh->bcfgCoop = BatchLaunch{};
+    if (pe->batched && b.split && !b.gbits && (b.lb == 8 || b.lb == 16) && tu.batchCoop >= 0) {
+        const int K = tu.batchCoop >= 2 ? std::min(tu.batchCoop, 8) : 2;
+        const int wpeC = tu.batchCoopWpe == 4 || tu.batchCoopWpe == 6 || tu.batchCoopWpe == 8
+                             ? tu.batchCoopWpe
+                             : ok8 ? 8 : ok6 ? 6 : 4;
+        BatchLaunch c2 = wpeC == 8 ? v8.first : wpeC == 6 ? v6.first : v4.first;
+        c2.split = 1;
+        const void* fn = batch_coop_kernel_ptr(b.lb, wpeC);
+        int per = 0;
+        if (c2.ldsBytes <= LDS &&
+            hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, c2.ldsBytes) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, c2.threads, c2.ldsBytes) == hipSuccess &&
+            per >= 1) {
+            c2.grid = sh->numCUs * per;
+            c2.coop = K;
+            const int64_t nB = ((int64_t)sh->rowCount + b.lb - 1) / b.lb;
+            if (tu.batchCoop >= 2 || (nB * K <= c2.grid && nB < b.grid)) sh->bcfgCoop = c2;
+        }
+        if (tu.batchCoop >= 2 && sh->bcfgCoop.grid > 0) {
+            sh->bcfg = sh->bcfgCoop;        // forced: the relax variant in use
+            sh->bcfgPost = b;
+            sh->bcfgAlt = sh->bcfgAlt2 = BatchLaunch{};
+        }
+    }
     sh->stats.deltaUsed = pe->batched ? b.delta : c.delta;
     sh->stats.batched = pe->batched ? 1 : 0;
     sh->stats.batchLanes = pe->batched ? b.lb : 0;
@@ -478,6 +514,7 @@ static void destroy_shard(Shard* s) {
         if (e) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->copyStream) (void)hipStreamDestroy(s->copyStream);
+    if (s->dCoopAbort) (void)hipHostFree(s->dCoopAbort);
 }
 
 // Upload the graph as a DevGraph.  oldOf == null: the caller's vertex ids.
@@ -863,7 +900,15 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     const size_t maxSlots = std::max<size_t>(1, (size_t)(budget / (double)perSlot));
     const size_t nBatchesAll = ((size_t)sh->rowCount + LB - 1) / LB;
     const size_t grid = (size_t)std::max({sh->bcfg.grid, sh->bcfgAlt.grid, sh->bcfgAlt2.grid});
-    const size_t slots = std::min<size_t>({grid, maxSlots, std::max<size_t>(1, nBatchesAll)});
+    // (a cooperative launch needs one slot per resident workgroup: its grid
+    // is the whole resident set, more workgroups than batches)
+    const size_t coGrid = sh->bcfgCoop.grid > 0 ? (size_t)sh->bcfgCoop.grid : 0;
+    const size_t slots = std::min<size_t>({std::max(grid, coGrid), maxSlots,
+                                          std::max<size_t>({(size_t)1, nBatchesAll, coGrid})});
+    if (coGrid > slots) {                          // scratch budget: no cooperative relax
+        if (sh->bcfg.coop >= 2) { sh->bcfg = sh->bcfgPost.grid > 0 ? sh->bcfgPost : sh->bcfg; sh->bcfg.coop = 0; }
+        sh->bcfgCoop = BatchLaunch{};
+    }
     sh->bcfg.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfg.grid);
     if (sh->bcfgAlt.grid > 0) sh->bcfgAlt.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt.grid);
     if (sh->bcfgAlt2.grid > 0) sh->bcfgAlt2.grid = (int32_t)std::min<size_t>(slots, (size_t)sh->bcfgAlt2.grid);
@@ -911,6 +956,26 @@ static int ensure_batch(ShdPe* pe, Shard* sh) {
     }
     sh->dBatchRows = (int32_t*)rows;
     sh->dBatchAmb = (uint8_t*)amb;
+    if (sh->bcfgCoop.grid > 0) {
+        // cooperative relax state: control words, one barrier line per group,
+        // two publication buffers of near bits + scalars per member per group
+        const size_t maxGroups = (size_t)sh->bcfgCoop.grid;
+        const size_t K = (size_t)sh->bcfgCoop.coop;
+        const size_t nwp = (size_t)batch_bits_words(pe->hg.n) / 2;
+        void *cc, *pub, *pubS;
+        if ((rc = dev_alloc(sh, &cc, 128 + maxGroups * 128)) ||
+            (rc = dev_alloc(sh, &pub, maxGroups * 2 * K * nwp * 4)) ||
+            (rc = dev_alloc(sh, &pubS, maxGroups * 2 * K * 16)))
+            return rc;
+        sh->bsc.coCtl = (int32_t*)cc;
+        sh->bsc.coBars = (int32_t*)cc + 32;
+        sh->bsc.coPub = (uint32_t*)pub;
+        sh->bsc.coPubS = (unsigned long long*)pubS;
+        sh->bsc.coK = (int32_t)K;
+        sh->bsc.coSpin = pe->tu.coopSpin;
+        if (hipHostMalloc(reinterpret_cast<void**>(&sh->dCoopAbort), 4, hipHostMallocDefault) != hipSuccess)
+            return SHD_PE_ENOMEM;
+    }
     if ((rc = ensure_tie(pe, sh))) return rc;
     sh->batchReady = true;
     return SHD_PE_OK;
@@ -1049,10 +1114,58 @@ static void corrupt_tie_slot(ShdPe* pe, Shard* sh, const std::vector<int32_t>& s
         if (!(thr[(size_t)sl] > 0.0)) continue;
         double* dd = sh->tie.D + (size_t)sl * (size_t)sh->tie.n;
         if (hipMemcpy(d.data(), dd, d.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-        for (double& x : d) x *= 0.5;
+        // 1: another source's array (halved distances); 2: an array whose
+        // own source is not at 0 (every distance shifted)
+        for (double& x : d) x = pe->tu.tieCorrupt == 2 ? x + 1.0 : x * 0.5;
         (void)hipMemcpy(dd, d.data(), d.size() * 8, hipMemcpyHostToDevice);
         return;
     }
+}
+
+// One round's relax by the cooperative kernel (K workgroups of one XCD per
+// batch): its control state zeroed and the round's per-batch failure flags
+// cleared by the host first.  If the runtime refuses the launch (the grid is
+// not wholly resident) or a barrier wait aborted, the plain relax recomputes
+// the round from scratch (it re-initialises every dist array it relaxes and
+// writes every flag): the rows are never wrong and never missing.
+// A cooperative launch takes every workgroup slot of its device: two of them
+// at once (logical shards of one device, computed by concurrent host
+// threads) could each hold part of the device while waiting for the rest of
+// their own grid.  One at a time per device (the launch is synchronised
+// before the lock is released, for the abort check anyway).
+static std::mutex g_coopMu[64];
+
+static int relax_coop(ShdPe* pe, Shard* sh, const BatchLaunch& relax, const int32_t* rows, int32_t rn,
+                      uint8_t* amb, int32_t* dbg) {
+    std::lock_guard<std::mutex> devLock(g_coopMu[sh->device & 63]);
+    const size_t maxGroups = (size_t)sh->bcfgCoop.grid;
+    HIPCHK(hipMemsetAsync(sh->bsc.coCtl, 0, 128 + maxGroups * 128, sh->stream));
+    HIPCHK(hipMemsetAsync(sh->bsc.flags, 0, (size_t)rn * 4, sh->stream));
+    BatchLaunch co = relax;
+    co.grid = std::min(co.grid, sh->batchSlots);
+    bool rerun = launch_batch_relax_coop(sh->dg, sh->tab, sh->bsc, rows, rn, amb, co, dbg, sh->dTie,
+                                         sh->stream) != 0;
+    if (rerun) {
+        (void)hipGetLastError();                  // the refusal
+    } else {
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(sh->dCoopAbort, sh->bsc.coCtl + 17, 4, hipMemcpyDeviceToHost, sh->stream));
+        HIPCHK(hipStreamSynchronize(sh->stream));
+        rerun = *sh->dCoopAbort != 0;
+    }
+    if (rerun) {
+        ++sh->coopAborts;
+        if (pe->tu.debug || pe->tu.tuneLog)
+            std::fprintf(stderr, "[shdpe] shard %d: cooperative relax %s; round recomputed by the plain relax\n",
+                         sh->gindex, *sh->dCoopAbort ? "aborted" : "refused");
+        BatchLaunch plain = relax;
+        plain.coop = 0;
+        plain.grid = std::min(plain.grid, sh->batchSlots);
+        HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
+        launch_batch_rows(sh->dg, sh->tab, sh->bsc, rows, rn, amb, plain, dbg, sh->dTie, sh->stream, 1);
+        HIPCHK(hipGetLastError());
+    }
+    return SHD_PE_OK;
 }
 
 // Compute the given table positions (all owned by `sh`), chunked.
@@ -1165,10 +1278,17 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                     const size_t ro = (size_t)r0 * LB;
                     if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[0], sh->stream));
                     for (int part = 1; part <= 2; ++part) {
-                        HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
-                        launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows + ro, rn,
-                                          sh->dBatchAmb + ro, part == 1 ? relax : post,
-                                          sh->dDbg ? sh->dDbg + 16 * r0 : nullptr, sh->dTie, sh->stream, part);
+                        int32_t* const dbgR = sh->dDbg ? sh->dDbg + 16 * r0 : nullptr;
+                        if (part == 1 && relax.coop >= 2 && sh->bcfgCoop.grid > 0) {
+                            if ((rc = relax_coop(pe, sh, relax, sh->dBatchRows + ro, rn, sh->dBatchAmb + ro,
+                                                 dbgR)))
+                                return rc;
+                        } else {
+                            HIPCHK(hipMemsetAsync(sh->bsc.next, 0, 4, sh->stream));
+                            launch_batch_rows(sh->dg, sh->tab, sh->bsc, sh->dBatchRows + ro, rn,
+                                              sh->dBatchAmb + ro, part == 1 ? relax : post, dbgR, sh->dTie,
+                                              sh->stream, part);
+                        }
                         if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[part], sh->stream));
                     }
                     if (sh->timeParts) {
@@ -1394,7 +1514,9 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
     std::lock_guard<std::mutex> lk(pe->mu);
     for (auto& sp : pe->shards) {
         Shard* sh = sp.get();
-        if (sh->tuned || (sh->bcfgAlt.grid <= 0 && sh->bcfgAlt2.grid <= 0) || sh->rowCount <= 0) continue;
+        if (sh->tuned || (sh->bcfgAlt.grid <= 0 && sh->bcfgAlt2.grid <= 0 && sh->bcfgCoop.grid <= 0) ||
+            sh->rowCount <= 0)
+            continue;
         // scratch first: ensure_batch sizes the slots and lowers the live
         // grids to them, and the candidates below are copies of those grids
         if (hipSetDevice(sh->device) != hipSuccess) return SHD_PE_EHIP;
@@ -1404,13 +1526,16 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
         std::vector<int32_t> pos(sh->rowCount);
         for (int32_t i = 0; i < sh->rowCount; ++i) pos[i] = sh->rowStart + i;
         const ShdPeStats keep = sh->stats;
-        double ms[3] = {0.0, 0.0, 0.0}, part[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-        int w[3] = {0, 0, 0};
-        BatchLaunch cand[3] = {sh->bcfg, sh->bcfgAlt, sh->bcfgAlt2};
+        double ms[4] = {0.0, 0.0, 0.0, 0.0}, part[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+        int w[4] = {0, 0, 0, 0};
+        BatchLaunch cand[4] = {sh->bcfg, sh->bcfgAlt, sh->bcfgAlt2, sh->bcfgCoop};
         const BatchLaunch orig[3] = {sh->bcfg, sh->bcfgAlt, sh->bcfgAlt2};
         int nc = 1;
         if (sh->bcfgAlt.grid > 0) cand[nc++] = sh->bcfgAlt;
         if (sh->bcfgAlt2.grid > 0) cand[nc++] = sh->bcfgAlt2;
+        // the cooperative relax (its post part runs the plain kernel of the
+        // same variant, so it is timed as that variant's post)
+        if (sh->bcfgCoop.grid > 0 && sh->bcfg.coop < 2 && sh->bcfg.split) cand[nc++] = sh->bcfgCoop;
         sh->bcfgPost = BatchLaunch{};
         for (int k = 0; k < nc; ++k) {
             sh->bcfg = cand[k];
@@ -1487,9 +1612,9 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
         sh->stats.batchPostWaves = sh->bcfg.split ? cand[pk].wpe : 0;
         if (pe->tu.debug || pe->tu.tuneLog)
             for (int k = 0; k < nc; ++k)
-                std::fprintf(stderr, "[shdpe] shard %d tune: %d waves %.2f ms (relax %.2f post %.2f)%s\n",
-                             sh->gindex, w[k], ms[k], part[k][0], part[k][1],
-                             k == nc - 1 ? (pk == rk ? " -> one variant" : " -> per part") : "");
+                std::fprintf(stderr, "[shdpe] shard %d tune: %d waves%s %.2f ms (relax %.2f post %.2f)%s%s\n",
+                             sh->gindex, w[k], cand[k].coop >= 2 ? " cooperative" : "", ms[k], part[k][0],
+                             part[k][1], k == rk ? " <relax" : "", k == pk ? " <post" : "");
         if ((pe->tu.debug || pe->tu.tuneLog) && relaxAlt > 0.0)
             std::fprintf(stderr, "[shdpe] shard %d tune: relax at 0.8 x delta %.2f ms vs %.2f -> delta %.3f\n",
                          sh->gindex, relaxAlt, relaxBase, relaxPick.delta);
@@ -2370,6 +2495,10 @@ extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
     // compute updates the per-shard stats under mu: snapshot under it too
     // (a call during a compute returns once that compute is done)
     std::lock_guard<std::mutex> lk(const_cast<ShdPe*>(pe)->mu);
+    for (auto& sp : pe->shards) {                // live per-shard counters into the stats
+        sp->stats.relaxCoopAborts = sp->coopAborts;
+        sp->stats.batchCoop = sp->bcfg.coop >= 2 ? sp->bcfg.coop : 0;
+    }
     ShdPeStats t = pe->shards[0]->stats;
     for (size_t i = 1; i < pe->shards.size(); ++i) {
         const ShdPeStats& s = pe->shards[i]->stats;
@@ -2377,6 +2506,7 @@ extern "C" int shd_pe_get_stats(const ShdPe* pe, ShdPeStats* out) {
         t.rowsExact += s.rowsExact;
         t.rowsTieEarly += s.rowsTieEarly;
         t.rowsTieRepaired += s.rowsTieRepaired;
+        t.relaxCoopAborts += s.relaxCoopAborts;
         t.arcsRelaxed += s.arcsRelaxed;
         t.msSparseKernel += s.msSparseKernel;
         t.msExactKernel += s.msExactKernel;
@@ -2424,6 +2554,7 @@ extern "C" int shd_pe_reset_stats(ShdPe* pe) {
         st.batchLanes = keep.batchLanes;
         st.batchWaves = keep.batchWaves;
         st.batchPostWaves = keep.batchPostWaves;
+        sp->coopAborts = 0;
     }
     pe->msGather = 0.0;
     return SHD_PE_OK;

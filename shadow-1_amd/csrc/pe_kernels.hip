@@ -1010,6 +1010,16 @@ __global__ __launch_bounds__(TW_THREADS) void k_tie_write(DevGraph g0, DevTable 
     if (tie_slot_bad(tie, slots[blockIdx.x])) return;   // the engine recomputes the row
     const size_t off = (size_t)slots[blockIdx.x] * (size_t)tie.n;
     const double* D = tie.D + off;
+    // latency floor: the exported distances must be this row's -- its own
+    // source at exactly 0 (latencies are validated > 0, so no other vertex
+    // is) -- or the row is not written from them: a slot filled from another
+    // source's array (the round-4 wrong-row symptom, latencies below the true
+    // distances) is marked bad and the engine recomputes the row with the
+    // full emulation (rowsTieRepaired)
+    if (D[s] != 0.0) {
+        if (tid == 0) tie.thr[slots[blockIdx.x]] = __builtin_nan("");
+        return;
+    }
     const int32_t* P = tie.P + off;
     int32_t* H = tie.H + off;
     double* R = tie.R + off;

@@ -71,7 +71,8 @@ class Stats(C.Structure):
                 ("denseSweeps", C.c_int64), ("denseFlops", C.c_double),
                 ("batched", C.c_int32), ("batchLanes", C.c_int32), ("nShards", C.c_int32),
                 ("msGather", C.c_double), ("rowsTieEarly", C.c_int64), ("batchWaves", C.c_int32),
-                ("batchPostWaves", C.c_int32), ("rowsTieRepaired", C.c_int64)]
+                ("batchPostWaves", C.c_int32), ("rowsTieRepaired", C.c_int64),
+                ("batchCoop", C.c_int32), ("relaxCoopAborts", C.c_int64)]
 
 
 class EngineError(RuntimeError):
@@ -164,7 +165,12 @@ def load_library(path: str = LIB_PATH):
         "shd_rowstore_adopt_image": (C.c_int, [vp, vp, i64, vp, vp, i64, f64]),
         "shd_pe_fill_rowstore": (C.c_int, [vp, vp, vp, vp]),
     }
+    # ABI-3 additions: an older build loaded through SHDPE_LIB (same-box A/B)
+    # lacks them; the in-tree library must have every symbol
+    optional = {"shd_pe_get_stats_sized", "shd_pe_stats_size"} if os.environ.get("SHDPE_LIB") else set()
     for name, (res, args) in sig.items():
+        if name in optional and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -744,16 +744,60 @@ def test_batched_kernel_each_lb(E, oracle_mod, monkeypatch, lb, wpe, case):
         assert st["rowsExact"] == 0
 
 
+@pytest.mark.parametrize("lb", [8, 16])
+@pytest.mark.parametrize("wpe", [4, 6, 8])
+@pytest.mark.parametrize("case", ["power_law", "quantized"])
+def test_cooperative_relax_each_variant(E, oracle_mod, monkeypatch, lb, wpe, case):
+    """The cooperative relax (two workgroups of one XCD share a batch: dist
+    array at agent scope, near bits published per listing round, group
+    barriers) forced at every batch width and variant it exists for: every
+    row bit-exact with the oracle, no batch failed its Bellman check (a lost
+    update would send it to the exact kernel), no launch aborted."""
+    monkeypatch.setenv("SHDPE_BATCH_LB", str(lb))
+    monkeypatch.setenv("SHDPE_BATCH_COOP", "2")
+    monkeypatch.setenv("SHDPE_BATCH_COOP_WPE", str(wpe))
+    if case == "power_law":
+        top = G.power_law(8000, m=3, seed=15)
+        att = G.sample_attached(top.n, 1203, seed=4)
+        srcs = att[::3]
+    else:
+        top, att, srcs = G.random_sparse(600, 6, seed=215, quantum=1.0), np.arange(599), None
+    st = _check_engine(E, oracle_mod, top, att, sources=srcs, force=5, debug_flags=E.DEBUG_ENV)
+    assert st["batched"] == 1 and st["batchLanes"] == lb and st["batchCoop"] == 2, st
+    assert st["relaxCoopAborts"] == 0, st
+    if case == "quantized":
+        assert st["rowsExact"] > 0, st
+    else:
+        assert st["rowsExact"] == 0, st
+
+
+def test_cooperative_relax_abort_recomputes(E, oracle_mod, monkeypatch):
+    """A cooperative launch whose barrier waits give up at once
+    (SHDPE_COOP_SPIN=0: the first wait that is not already satisfied aborts
+    the launch) is recomputed by the plain relax: the aborts are counted and
+    every row is still bit-exact -- never a wrong or missing row."""
+    monkeypatch.setenv("SHDPE_BATCH_LB", "8")
+    monkeypatch.setenv("SHDPE_BATCH_COOP", "2")
+    monkeypatch.setenv("SHDPE_COOP_SPIN", "0")
+    top = G.power_law(8000, m=3, seed=15)
+    att = G.sample_attached(top.n, 1203, seed=4)
+    st = _check_engine(E, oracle_mod, top, att, sources=att[::3], force=5, debug_flags=E.DEBUG_ENV)
+    assert st["batchCoop"] == 2 and st["relaxCoopAborts"] >= 1 and st["rowsExact"] == 0, st
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("case", ["batched", "sparse"])
-def test_tie_slot_cross_check_repairs(E, oracle_mod, monkeypatch, case):
+def test_tie_slot_cross_check_repairs(E, oracle_mod, monkeypatch, case, mode):
     """Early-stop tie rows: the exact kernel checks every vertex it popped
     against the exported distance of the same row (a slot holding another
     source's or a stale distance array -- the round-4 r04t symptom, latencies
-    below the true distance -- fails it).  SHDPE_TIE_CORRUPT halves one
-    slot's exported distances after the relevance scan: the row must be
-    caught (rowsTieRepaired), recomputed by the full emulation, and every row
-    stays bit-exact with the oracle."""
-    monkeypatch.setenv("SHDPE_TIE_CORRUPT", "1")
+    below the true distance -- fails it), and k_tie_write writes no row from
+    an array whose own source is not at distance 0 (the latency floor).
+    SHDPE_TIE_CORRUPT=1 halves one slot's exported distances after the
+    relevance scan, =2 shifts them all by 1 ms: the row must be caught
+    (rowsTieRepaired), recomputed by the full emulation, and every row stays
+    bit-exact with the oracle."""
+    monkeypatch.setenv("SHDPE_TIE_CORRUPT", mode)
     if case == "batched":
         top, att, force = G.random_sparse(600, 6, seed=216, quantum=1.0), np.arange(599), 5
     else:

@@ -150,15 +150,19 @@ def test_c4_two_shards_full_size(E, c4_one):
     two.close()
 
 
-@pytest.mark.parametrize("wpe", ["tune", "4", "8"])
+@pytest.mark.parametrize("wpe", ["tune", "4", "8", "coop"])
 def test_c4_eight_shards_full_size(E, c4_one, monkeypatch, wpe):
     """C4 in eight logical shards = what each rank of the 8-GPU run computes
     (2,048 rows, LB 8 batches, the tune's variant pick -- and each of the two
-    variants forced): whole table byte-identical to one engine's, before and
+    variants forced, and the cooperative relax forced: two workgroups of one
+    XCD per batch): whole table byte-identical to one engine's, before and
     after the gather, and the device fingerprints agree."""
     top, att, one, ck = c4_one
     dbg = 0
-    if wpe != "tune":
+    if wpe == "coop":
+        monkeypatch.setenv("SHDPE_BATCH_COOP", "2")
+        dbg = E.DEBUG_ENV
+    elif wpe != "tune":
         monkeypatch.setenv("SHDPE_BATCH_WPE", wpe)
         dbg = E.DEBUG_ENV
     eng = E.Engine(top, att, devices=[0] * 8, debug_flags=dbg)
@@ -169,8 +173,11 @@ def test_c4_eight_shards_full_size(E, c4_one, monkeypatch, wpe):
     eng.compute_all()
     st = eng.stats()
     assert st["batched"] == 1 and st["batchLanes"] == 8 and st["rowsExact"] == 0, st
-    if wpe != "tune":
-        assert st["batchWaves"] == int(wpe)
+    assert st["rowsTieRepaired"] == 0 and st["relaxCoopAborts"] == 0, st
+    if wpe == "coop":
+        assert st["batchCoop"] == 2, st
+    elif wpe != "tune":
+        assert st["batchWaves"] == int(wpe) and st["batchCoop"] == 0
     _same_blocks(one, eng, f"c4 x8 wpe {wpe}")
     eng.gather()
     assert np.array_equal(eng.row_checksums(0, eng.T), ck)

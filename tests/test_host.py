@@ -50,7 +50,7 @@ def test_stats_struct_size_matches_binding(lib):
     import ctypes
     from shdpe.engine import Stats
     assert lib.shd_pe_stats_size() == ctypes.sizeof(Stats)
-    assert Stats._fields_[-1][0] == "rowsTieRepaired"
+    assert Stats._fields_[-1][0] == "relaxCoopAborts"
 
 
 def test_library_is_gfx950_code_object():

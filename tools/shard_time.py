@@ -25,7 +25,8 @@ for N in [int(x) for x in sys.argv[2:]]:
         best = min(best, time.perf_counter() - t)
     st = eng.stats()
     print(f"{wl} N={N} rows={cnt} ms={best*1e3:.1f} lanes={st['batchLanes']} "
-          f"waves={st['batchWaves']}/{st['batchPostWaves']} "
+          f"waves={st['batchWaves']}/{st['batchPostWaves']} coop={st.get('batchCoop', 0)} "
+          f"aborts={st.get('relaxCoopAborts', 0)} exact={st['rowsExact']} "
           f"rows/s/gpu={cnt/best:.0f} -> {N*cnt/best:.0f} total "
           f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('SHDPE_'))}]", flush=True)
     eng.close()
