@@ -263,7 +263,9 @@ int shd_pe_gather(ShdPe* pe);
 /* Cross-process RCCL communicator, one rank per engine (nDevices == 1,
  * rank = shardIndex, nranks = shardCount): one process makes the id, the
  * host's own channel (MPI, a socket, torch.distributed) hands its bytes to
- * every process, each calls shd_pe_comm_init. */
+ * every process, each calls shd_pe_comm_init.  shardCount 1 is accepted (a
+ * one-rank communicator: the gather issues the same RCCL calls, an in-place
+ * all-gather of the engine's own rows). */
 int shd_pe_comm_unique_id(void* out, int32_t bytes);   /* bytes >= 128 */
 int shd_pe_comm_init(ShdPe* pe, const void* uniqueId, int32_t bytes);
 /* Host-transport assembly, the alternative to shd_pe_gather where RCCL has no

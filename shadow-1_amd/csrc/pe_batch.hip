@@ -102,8 +102,17 @@ constexpr int BCTRL_BYTES = 128;
 // pass ran (attempt 1), 128 the relax kernel flagged the batch (phase cap)
 #ifdef SHDPE_DIAG_WHY
 #define DIAG_WHY(bit) (why |= (bit))
+// the first phase-2 violations of the first batches: entry, stored distance,
+// the in-arc minimum that undercuts it (printf; diagnostic builds only)
+#define DIAG_VIOL(b, v, lane, dv, mnv, hv)                                                     \
+    do {                                                                                    \
+        if ((b) < 6 && atomicAdd(&sDiagViol, 1) < 4)                                        \
+            printf("[diag] viol batch %d v %d lane %d dist %.17g min %.17g heavy %d attempt %d\n", \
+                   (b), (v), (lane), b2d(dv), b2d(mnv), (hv), attempt);                     \
+    } while (0)
 #else
 #define DIAG_WHY(bit) ((void)0)
+#define DIAG_VIOL(b, v, lane, dv, mnv, hv) ((void)0)
 #endif
 
 // Entry encoding of the [v][LB] distance array: (f64 bits << 1) | dirty.
@@ -493,6 +502,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         if constexpr (PT == 2) failed = as_global(bs.flags)[b] != 0;
 #ifdef SHDPE_DIAG_WHY
         uint32_t why = failed ? 128u : 0u;
+        __shared__ int sDiagViol;
+        if (tid == 0) sDiagViol = 0;
+        __syncthreads();
 #endif
         uint32_t needMask = 0u;
         for (int attempt = 0;; ++attempt) {
@@ -1072,6 +1084,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     if (bad) {
                         D[e] = enc_dirty(mn[v]);
                         viol = 1;
+                        DIAG_VIOL(b, vv, l, dC[v], mn[v], 0);
                     }
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
                     if (bm && l == 0) anyC.set(vv);
@@ -1188,6 +1201,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                     if (bad && gw == 0) {
                         D[e] = enc_dirty(mn);
                         viol = 1;
+                        DIAG_VIOL(b, vv, l, dv, mn, 1);
                     }
                     const uint32_t bm = (uint32_t)(__ballot(bad) >> gbase) & LBMASK;
                     if (bm && l == 0 && gw == 0) anyC.set(vv);

@@ -94,7 +94,7 @@ struct Tuning {
     int tieCorrupt = 0;        // tests only: scale one early-stop slot's exported distances
                                // after the relevance scan (exercises the tie-slot repair)
     int batchCoop = 0;         // cooperative relax: K workgroups per batch (>= 2 forces it,
-                               // 0 = the tune decides, -1 = never)
+                               // 1 = a shd_pe_tune candidate, 0 = off)
     int batchCoopWpe = 0;      // its variant (8 / 6 / 4 waves; 0 = the one with two
                                // workgroups per CU)
     int coopSpin = 1 << 22;    // its barrier poll limit (tests shrink it to force aborts)

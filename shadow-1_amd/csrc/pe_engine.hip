@@ -366,9 +366,11 @@ static int configure(ShdPe* pe, Shard* sh) {
     // shard with fewer batches than the plain relax has workgroup slots --
     // the C4 8-GPU shard's 256 LB-8 batches leave one of the two 8-wave
     // slots of every CU idle -- the batch's listing rounds are shared by K
-    // workgroups.  A candidate of shd_pe_tune; SHDPE_BATCH_COOP=K forces it.
+    // workgroups.  SHDPE_BATCH_COOP=K forces it, =1 makes it a candidate of
+    // shd_pe_tune (off by default: slower than the plain relax wherever it
+    // was measured).
     sh->bcfgCoop = BatchLaunch{};
-    if (pe->batched && b.split && !b.gbits && (b.lb == 8 || b.lb == 16) && tu.batchCoop >= 0) {
+    if (pe->batched && b.split && !b.gbits && (b.lb == 8 || b.lb == 16) && tu.batchCoop >= 1) {
         const int K = tu.batchCoop >= 2 ? std::min(tu.batchCoop, 8) : 2;
         const int wpeC = tu.batchCoopWpe == 4 || tu.batchCoopWpe == 6 || tu.batchCoopWpe == 8
                              ? tu.batchCoopWpe
@@ -384,7 +386,11 @@ static int configure(ShdPe* pe, Shard* sh) {
             c2.grid = sh->numCUs * per;
             c2.coop = K;
             const int64_t nB = ((int64_t)sh->rowCount + b.lb - 1) / b.lb;
-            if (tu.batchCoop >= 2 || (nB * K <= c2.grid && nB < b.grid)) sh->bcfgCoop = c2;
+            // a tune candidate only on request (SHDPE_BATCH_COOP=1): measured
+            // slower than the plain relax at every shard size (round 6, C4
+            // N=8: 17.1-22.6 vs 16.8 ms; profiles/r06_shard_times.txt)
+            if (tu.batchCoop >= 2 || (tu.batchCoop == 1 && nB * K <= c2.grid && nB < b.grid))
+                sh->bcfgCoop = c2;
         }
         if (tu.batchCoop >= 2 && sh->bcfgCoop.grid > 0) {
             sh->bcfg = sh->bcfgCoop;        // forced: the relax variant in use
@@ -2165,7 +2171,7 @@ static int gather_locked(ShdPe* pe) {
     HIPCHK(hipEventCreate(&ev.e[1]));
     hipEvent_t e0 = ev.e[0], e1 = ev.e[1];
     HIPCHK(hipEventRecord(e0, s0->stream));
-    if (pe->G == 1) {
+    if (pe->G == 1 && !pe->xcomm) {
         // nothing to exchange
     } else if (pe->xcomm) {
         // cross-process: every process owns one shard (nDevices == 1), rows
@@ -2323,7 +2329,10 @@ extern "C" int shd_pe_comm_unique_id(void* out, int32_t bytes) {
 
 extern "C" int shd_pe_comm_init(ShdPe* pe, const void* uniqueId, int32_t bytes) {
     if (!pe || !uniqueId || bytes < (int32_t)sizeof(ncclUniqueId)) return SHD_PE_EINVAL;
-    if (pe->opt.nDevices != 1 || pe->opt.shardCount < 2) return SHD_PE_EINVAL;
+    // (shardCount 1: a one-rank communicator -- the gather then runs the same
+    // RCCL calls as at N > 1, an in-place all-gather of the engine's own
+    // rows: how the RCCL path is exercised on a one-GPU box)
+    if (pe->opt.nDevices != 1 || pe->opt.shardCount < 1) return SHD_PE_EINVAL;
     std::lock_guard<std::mutex> lk(pe->mu);
     if (pe->xcomm) return SHD_PE_OK;
     ncclUniqueId id;

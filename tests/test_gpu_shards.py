@@ -9,8 +9,10 @@ What runs where:
   * the RCCL gathers (in-process ncclCommInitAll over distinct devices, and
     the cross-process communicator of shd_pe_comm_init) need one device per
     rank: test_rccl_gather_distinct_devices runs only when >= 2 GPUs are
-    visible and is skipped on the 1-GPU test box, so those code paths are
-    NOT verified on hardware by this suite.
+    visible and is skipped on the 1-GPU test box; the cross-process calls
+    (ncclCommInitRank, the per-field ncclAllGather group) run on one GPU
+    through a one-rank communicator (test_rccl_one_rank_communicator_gather),
+    the multi-rank exchange itself is NOT verified on hardware by this suite.
 """
 import os
 import sys
@@ -335,6 +337,28 @@ def _visible_gpus():
         return torch.cuda.device_count()
     except Exception:          # noqa: BLE001 - no torch / no ROCm runtime
         return 0
+
+
+def test_rccl_one_rank_communicator_gather(E):
+    """The cross-process RCCL path on one GPU: a one-rank communicator
+    (shd_pe_comm_unique_id + shd_pe_comm_init with shardCount 1) makes
+    shd_pe_gather issue the calls an N-rank run does (ncclCommInitRank, a
+    group of one ncclAllGather per field, in place); every field is still
+    byte-identical to an engine that never gathered, and the gather was
+    timed (it ran)."""
+    top, att, force = _shard_case("batched")
+    one = E.Engine(top, att, force_mode=force)
+    one.compute_all()
+    ref = _all_rows(one)
+    one.close()
+    eng = E.Engine(top, att, force_mode=force, shard_index=0, shard_count=1)
+    eng.comm_init(E.Engine.comm_unique_id())
+    eng.compute_all()
+    eng.gather()
+    _same(_all_rows(eng), ref, "rccl one-rank gathered")
+    st = eng.stats()
+    assert st["nShards"] == 1 and st["msGather"] > 0, st
+    eng.close()
 
 
 def test_rccl_gather_distinct_devices(E):
