@@ -89,6 +89,7 @@ struct Tuning {
     double batchDeltaFactor = 0.75, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
+    int densePredCm = 0;       // dense predecessor pass: chunk-minimum test (MP_PRED_CM)
     int debug = 0, streamWgPerCU = 16;
     int tuneLog = 0;           // print shd_pe_tune's per-variant times (no kernel counters)
     int tieCorrupt = 0;        // tests only: scale one early-stop slot's exported distances
@@ -98,6 +99,9 @@ struct Tuning {
     int batchCoopWpe = 0;      // its variant (8 / 6 / 4 waves; 0 = the one with two
                                // workgroups per CU)
     int coopSpin = 1 << 22;    // its barrier poll limit (tests shrink it to force aborts)
+    int failWpe = 0;           // tests only: the relax variant of this wave count flags
+                               // every batch failed (a miscompiled variant; shd_pe_tune
+                               // must not pick it)
 };
 
 struct DevScratch {

@@ -181,10 +181,12 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gd("SHDPE_DENSE_MIN", t.denseMin);
     gd("SHDPE_DENSE_BATCH_GB", t.denseBatchGB);
     gi("SHDPE_PRED_MI", t.densePredMi);
+    gi("SHDPE_PRED_CM", t.densePredCm);
     gi("SHDPE_DENSE_EPOCHS", t.denseEpochs);
     gi("SHDPE_DEBUG", t.debug);
     gi("SHDPE_STREAM_WG_PER_CU", t.streamWgPerCU);
     gi("SHDPE_TIE_CORRUPT", t.tieCorrupt);
+    gi("SHDPE_TUNE_FAIL_WPE", t.failWpe);
     gi("SHDPE_TUNE_LOG", t.tuneLog);
     gi("SHDPE_BATCH_COOP", t.batchCoop);
     gi("SHDPE_BATCH_COOP_WPE", t.batchCoopWpe);
@@ -1295,6 +1297,10 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                                               sh->dBatchAmb + ro, part == 1 ? relax : post, dbgR, sh->dTie,
                                               sh->stream, part);
                         }
+                        // tests only (SHDPE_TUNE_FAIL_WPE): the relax variant of that wave
+                        // count flags every batch failed, as a miscompiled variant would
+                        if (part == 1 && pe->tu.failWpe && relax.wpe == pe->tu.failWpe)
+                            HIPCHK(hipMemsetAsync(sh->bsc.flags, 1, (size_t)rn * 4, sh->stream));
                         if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[part], sh->stream));
                     }
                     if (sh->timeParts) {
@@ -1534,6 +1540,7 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
         const ShdPeStats keep = sh->stats;
         double ms[4] = {0.0, 0.0, 0.0, 0.0}, part[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
         int w[4] = {0, 0, 0, 0};
+        int64_t ex[4] = {0, 0, 0, 0};   // rows each candidate sent to the exact path
         BatchLaunch cand[4] = {sh->bcfg, sh->bcfgAlt, sh->bcfgAlt2, sh->bcfgCoop};
         const BatchLaunch orig[3] = {sh->bcfg, sh->bcfgAlt, sh->bcfgAlt2};
         int nc = 1;
@@ -1550,6 +1557,7 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
             // second is timed (split kernels: relax and post separately)
             for (int rep = 0; rep < 2; ++rep) {
                 const double m0 = sh->stats.msSparseKernel;
+                const int64_t x0 = sh->stats.rowsExact;
                 sh->msPart[0] = sh->msPart[1] = 0.0;
                 sh->timeParts = rep == 1 && sh->bcfg.split;
                 int rc = compute_shard(pe, sh, pos.data(), sh->rowCount);
@@ -1562,14 +1570,30 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
                 ms[k] = sh->stats.msSparseKernel - m0;
                 part[k][0] = sh->msPart[0];
                 part[k][1] = sh->msPart[1];
+                ex[k] = sh->stats.rowsExact - x0;
             }
         }
+        // Every variant computes the same rows, so they all send the same
+        // rows to the exact path -- except one whose batches fail their
+        // checks (a miscompiled instantiation: round 6 found one whose post
+        // kernel failed every batch's Bellman check under one register
+        // allocation).  Such a variant looks FASTER here (its
+        // skipped phases are not in the batch-kernel time, the exact kernel
+        // is), so it is never picked: only candidates at the fewest exact
+        // rows compete.
+        int64_t exMin = ex[0];
+        for (int k = 1; k < nc; ++k) exMin = std::min(exMin, ex[k]);
+        bool ok[4] = {false, false, false, false};
+        for (int k = 0; k < nc; ++k) ok[k] = ex[k] == exMin;
         // whole launches, or per part when every variant ran split: the
         // relax kernel and the post kernel each take their fastest variant
         bool perPart = true;
         for (int k = 0; k < nc; ++k) perPart = perPart && cand[k].split && part[k][0] > 0.0;
-        int rk = 0, pk = 0;
-        for (int k = 1; k < nc; ++k) {
+        int rk = 0;
+        while (!ok[rk]) ++rk;
+        int pk = rk;
+        for (int k = rk + 1; k < nc; ++k) {
+            if (!ok[k]) continue;
             if (perPart ? part[k][0] < part[rk][0] : ms[k] < ms[rk]) rk = k;
             if (perPart ? part[k][1] < part[pk][1] : ms[k] < ms[pk]) pk = k;
         }
@@ -1618,9 +1642,10 @@ extern "C" int shd_pe_tune(ShdPe* pe) {
         sh->stats.batchPostWaves = sh->bcfg.split ? cand[pk].wpe : 0;
         if (pe->tu.debug || pe->tu.tuneLog)
             for (int k = 0; k < nc; ++k)
-                std::fprintf(stderr, "[shdpe] shard %d tune: %d waves%s %.2f ms (relax %.2f post %.2f)%s%s\n",
+                std::fprintf(stderr, "[shdpe] shard %d tune: %d waves%s %.2f ms (relax %.2f post %.2f) exact rows %ld%s%s%s\n",
                              sh->gindex, w[k], cand[k].coop >= 2 ? " cooperative" : "", ms[k], part[k][0],
-                             part[k][1], k == rk ? " <relax" : "", k == pk ? " <post" : "");
+                             part[k][1], (long)ex[k], ok[k] ? "" : " (excluded)", k == rk ? " <relax" : "",
+                             k == pk ? " <post" : "");
         if ((pe->tu.debug || pe->tu.tuneLog) && relaxAlt > 0.0)
             std::fprintf(stderr, "[shdpe] shard %d tune: relax at 0.8 x delta %.2f ms vs %.2f -> delta %.3f\n",
                          sh->gindex, relaxAlt, relaxBase, relaxPick.delta);

@@ -698,6 +698,33 @@ def test_tune_picks_a_variant_and_keeps_parity(E, oracle_mod):
 
 
 @pytest.mark.parametrize("wpe", [4, 6, 8])
+def test_tune_never_picks_a_failing_variant(E, oracle_mod, monkeypatch, wpe):
+    """A variant whose batches fail their checks (SHDPE_TUNE_FAIL_WPE: its
+    relax flags every batch, as the miscompiled post kernel of round 6's
+    r05au record did) looks faster to the tune -- its skipped phases are not
+    in the batch-kernel time -- but sends every row to the exact path: the
+    tune excludes it for both kernels, and the table it leaves is computed
+    on the fast path, bit-exact."""
+    monkeypatch.setenv("SHDPE_TUNE_FAIL_WPE", str(wpe))
+    top = G.power_law(8000, m=3, seed=14)
+    att = G.sample_attached(top.n, 1200, seed=3)
+    eng = E.Engine(top, att, force_mode=5, debug_flags=E.DEBUG_ENV)
+    eng.tune()
+    st = eng.stats()
+    assert st["batched"] == 1 and st["batchWaves"] != wpe and st["batchPostWaves"] != wpe, st
+    eng.compute_all()
+    st = eng.stats()
+    assert st["rowsExact"] == 0, st
+    og = oracle_mod.OracleGraph(top)
+    pos = np.arange(0, eng.T, 37)
+    exp = og.rows(eng.attached[pos], eng.attached, threads=8)
+    for i, p in enumerate(pos):
+        got = {k: (v[0] if v is not None else None) for k, v in eng.get_rows(int(p), 1).items()}
+        _assert_rows_equal(got, {k: v[i] for k, v in exp.items()}, f"row {p}")
+    eng.close()
+
+
+@pytest.mark.parametrize("wpe", [4, 6, 8])
 @pytest.mark.parametrize("case", ["power_law", "quantized"])
 def test_batched_kernel_each_variant(E, oracle_mod, monkeypatch, wpe, case):
     """Every k_batch_rows variant the tune may pick (4 / 6 / 8 waves per

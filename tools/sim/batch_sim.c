@@ -27,6 +27,18 @@ typedef struct {
     double impvOver[4]; // phases with more than 128 / 256 / 512 / 1024 improved vertices
 } SimOut;
 
+static const double* g_sortKey;
+// hub-cache probe (sim_set_hubs): arc visits / improving visits whose head,
+// and vertex processings whose tail, is a marked hub
+static const uint8_t* g_hub;
+double g_hubArcs, g_hubImp, g_hubProcs;
+void sim_set_hubs(const uint8_t* h) { g_hub = h; g_hubArcs = g_hubImp = g_hubProcs = 0; }
+void sim_hub_counts(double* o) { o[0] = g_hubArcs; o[1] = g_hubImp; o[2] = g_hubProcs; }
+static int cmp_key(const void* a, const void* b) {
+    const double x = g_sortKey[*(const int32_t*)a], y = g_sortKey[*(const int32_t*)b];
+    return x < y ? -1 : x > y ? 1 : 0;
+}
+
 // vkey (optional, [nBatch][n]): a per-VERTEX bucket key replacing every
 // lane's dist - off (scheduling experiments: all lanes of a vertex processed
 // together at the vertex's key).
@@ -43,6 +55,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     int farNext = 0;                 // something entered farp (the next bucket) this bucket
     int32_t* stamp = malloc(sizeof(int32_t) * n);
     int32_t* istamp = malloc(sizeof(int32_t) * n);   // improved in phase gphase
+    double* sortKey = malloc(sizeof(double) * n);      // farMode & 16: light-queue order
     uint64_t* hpend = calloc(n, 8);   // lanes whose heavy arcs wait for their bucket to settle
     for (int v = 0; v < n; ++v) stamp[v] = istamp[v] = -1;
     uint8_t* recP = calloc(n, 1);   // all lanes below the bound when last processed (this bucket)
@@ -86,8 +99,24 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
             int qn = 0;
             for (int v = 0; v < n; ++v)
                 if (pend[v] && rowPtr[v + 1] - rowPtr[v] >= heavyDeg) q[qn++] = v;
+            const int qh = qn;
             for (int v = 0; v < n; ++v)
                 if (pend[v] && rowPtr[v + 1] - rowPtr[v] < heavyDeg) q[qn++] = v;
+            if (farMode & 16) {
+                // within-phase order: light candidates by their smallest dirty
+                // lane key (the order a per-phase key sort would give)
+                g_sortKey = sortKey;
+                for (int i = qh; i < qn; ++i) {
+                    const int v = q[i];
+                    double mk = INFINITY;
+                    for (int l = 0; l < LB; ++l) {
+                        const double d = D[(size_t)v * LB + l];
+                        if (d != INFINITY && ((dirty[v] >> l) & 1)) { const double k = KEY(v, l, d); if (k < mk) mk = k; }
+                    }
+                    sortKey[v] = mk;
+                }
+                qsort(q + qh, qn - qh, sizeof(int32_t), cmp_key);
+            }
             if (qn == 0 && (farMode & 4)) {
                 // bucket settled: heavy arcs (w >= delta) of the lanes whose
                 // key is below the bound, once, with their final values
@@ -189,6 +218,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                 if (!act) continue;
                 dirty[u] &= ~act;
                 out->procs += 1;
+                if (g_hub && g_hub[u]) g_hubProcs += 1;
                 {
                     int all = 1;
                     for (int l = 0; l < LB; ++l)
@@ -212,6 +242,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                         out->skip2 += recF[x];
                     }
                     if (stamp[x] != gphase) { stamp[x] = gphase; out->touched += 1; }
+                    if (g_hub && g_hub[x]) g_hubArcs += 1;
                     int anyImp = 0;
                     for (int l = 0; l < LB; ++l) {
                         if (!((act >> l) & 1)) continue;
@@ -232,6 +263,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
                         }
                     }
                     out->improving += anyImp;
+                    if (g_hub && g_hub[x]) g_hubImp += anyImp;
                 }
             }
             memcpy(pend, nextp, n);
@@ -256,6 +288,7 @@ int batch_sim(int32_t n, const int32_t* rowPtr, const int32_t* col, const double
     free(farp2);
     free(stamp);
     free(istamp);
+    free(sortKey);
     free(hpend);
     free(recP);
     free(recF);
