@@ -79,7 +79,7 @@ constexpr int MJ = 8;          // targets per thread
 constexpr int TCOL = 16 * MJ;  // 128 targets per tile
 constexpr int KB = 16;         // K chunk
 constexpr int MAXCH = 4096;    // chunk list capacity (n <= 65536 uses chunk epochs)
-enum { MP_SWEEP = 0, MP_PRED = 1, MP_PRED_CM = 2 };
+enum { MP_SWEEP = 0, MP_PRED = 1 };
 
 template <int MODE, int MI>
 __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, double* D, int64_t n,
@@ -164,21 +164,14 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
     };
 
     double acc[MI][MJ];     // SWEEP: running min; PRED: target distance
-    constexpr bool PRED = MODE != MP_SWEEP;
-    double best[PRED ? MI : 1][MJ];
-    int arg[PRED ? MI : 1][MJ];   // -1 none, >= 0 unique, -2 tie
-    // MP_PRED_CM: the running minimum of a + b over the K chunk; a tight u
-    // exists in the chunk iff it equals the target distance (every a + b is
-    // >= D[s][v] at the fixpoint), and only then is the chunk re-scanned
-    // from LDS for that entry -- per relaxation the sweep's add + min
-    // instead of an add, a compare and a wave-wide test
-    double cmin[MODE == MP_PRED_CM ? MI : 1][MJ];
+    double best[MODE == MP_PRED ? MI : 1][MJ];
+    int arg[MODE == MP_PRED ? MI : 1][MJ];   // -1 none, >= 0 unique, -2 tie
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
         const int r = r0 + ty + 16 * i;
 #pragma unroll
         for (int j = 0; j < MJ; ++j) {
-            if constexpr (MODE == MP_SWEEP) {
+            if (MODE == MP_SWEEP) {
                 acc[i][j] = DINF;
             } else {
                 const int64_t v = v0 + tx + 16 * j;
@@ -199,12 +192,6 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
         for (int q = 0; q < KB / 2; ++q) Bs[bK + 2 * q][bC] = rb[q];
         __syncthreads();
         if (c + 1 < nVisit) fetch(chunkK(c + 1));
-        if constexpr (MODE == MP_PRED_CM) {
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-                for (int j = 0; j < MJ; ++j) cmin[i][j] = DINF;
-        }
 #pragma unroll 4
         for (int kk = 0; kk < KB; ++kk) {
             double a[MI], b[MJ];
@@ -212,17 +199,12 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
             for (int i = 0; i < MI; ++i) a[i] = At[kk][ty + 16 * i];
 #pragma unroll
             for (int j = 0; j < MJ; ++j) b[j] = Bs[kk][tx + 16 * j];
-            if constexpr (MODE == MP_PRED_CM) {
-#pragma unroll
-                for (int i = 0; i < MI; ++i)
-#pragma unroll
-                    for (int j = 0; j < MJ; ++j) cmin[i][j] = fmin(cmin[i][j], a[i] + b[j]);
-            } else if (MODE == MP_SWEEP) {
+            if (MODE == MP_SWEEP) {
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
                     for (int j = 0; j < MJ; ++j) acc[i][j] = fmin(acc[i][j], a[i] + b[j]);
-            } else if constexpr (MODE == MP_PRED) {
+            } else {
                 bool hit = false;
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
@@ -242,36 +224,9 @@ __global__ __launch_bounds__(256) void k_minplus(DevGraph g, const double* W, do
                 }
             }
         }
-        if constexpr (MODE == MP_PRED_CM) {
-            // entries with a tight u in this chunk (rare: about one chunk in
-            // n / KB per entry) re-scan it in u order, exactly as MP_PRED
-            // does per k step (the chunk is still in LDS)
-            bool hit = false;
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-                for (int j = 0; j < MJ; ++j) hit |= cmin[i][j] == acc[i][j] && acc[i][j] < DINF;
-            if (__any(hit)) {
-#pragma unroll
-                for (int i = 0; i < MI; ++i)
-#pragma unroll
-                    for (int j = 0; j < MJ; ++j) {
-                        if (!(cmin[i][j] == acc[i][j] && acc[i][j] < DINF)) continue;
-#pragma unroll 1
-                        for (int kk = 0; kk < KB; ++kk) {
-                            const double a = At[kk][ty + 16 * i];
-                            if (a + Bs[kk][tx + 16 * j] == acc[i][j]) {
-                                const int u = (int)(k0 + kk);
-                                if (a < best[i][j]) { best[i][j] = a; arg[i][j] = u; }
-                                else if (a == best[i][j]) arg[i][j] = -2;
-                            }
-                        }
-                    }
-            }
-        }
     }
 
-    if constexpr (MODE == MP_SWEEP) {
+    if (MODE == MP_SWEEP) {
         int changed = 0;
         int colCh = 0;      // bit j: some row of mine changed in chunk v0/16 + j
 #pragma unroll
@@ -442,17 +397,7 @@ int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, c
         }
         if (!any || sweeps > n) break;
     }
-    if (tu.densePredCm && (miP == 2 || miP == 3 || miP == 4)) {
-        if (miP == 2)
-            hipLaunchKernelGGL((k_minplus<MP_PRED_CM, 2>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
-                               rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
-        else if (miP == 3)
-            hipLaunchKernelGGL((k_minplus<MP_PRED_CM, 3>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
-                               rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
-        else
-            hipLaunchKernelGGL((k_minplus<MP_PRED_CM, 4>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
-                               rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
-    } else if (miP == 6)
+    if (miP == 6)
         hipLaunchKernelGGL((k_minplus<MP_PRED, 6>), gridP, dim3(256), 0, st, g, W, D, n, ldD, nRows,
                            rowActive, rowChanged, dAny, dRows, P, rowAmb, chunkEpoch, 0);
     else if (miP == 3)

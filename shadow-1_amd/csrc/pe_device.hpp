@@ -89,7 +89,6 @@ struct Tuning {
     double batchDeltaFactor = 0.75, batchScratchGB = 64.0;
     double denseMin = 0.25, denseBatchGB = 24.0;
     int densePredMi = 2, denseEpochs = 1;
-    int densePredCm = 0;       // dense predecessor pass: chunk-minimum test (MP_PRED_CM)
     int debug = 0, streamWgPerCU = 16;
     int tuneLog = 0;           // print shd_pe_tune's per-variant times (no kernel counters)
     int tieCorrupt = 0;        // tests only: scale one early-stop slot's exported distances

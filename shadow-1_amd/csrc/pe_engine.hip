@@ -181,7 +181,6 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gd("SHDPE_DENSE_MIN", t.denseMin);
     gd("SHDPE_DENSE_BATCH_GB", t.denseBatchGB);
     gi("SHDPE_PRED_MI", t.densePredMi);
-    gi("SHDPE_PRED_CM", t.densePredCm);
     gi("SHDPE_DENSE_EPOCHS", t.denseEpochs);
     gi("SHDPE_DEBUG", t.debug);
     gi("SHDPE_STREAM_WG_PER_CU", t.streamWgPerCU);
