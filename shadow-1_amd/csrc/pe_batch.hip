@@ -388,7 +388,12 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
     const int n = g.n;
     const int nw = (n + 31) >> 5;
     const int nwp = (nw + 3) & ~3;
-    const int tid = threadIdx.x, NT = blockDim.x;
+    // the workgroup size is part of the variant (launch_lb checks it): a
+    // compile-time NT makes every stride, group count and LDS tile offset a
+    // constant instead of a live register (round 6: fewer spills in the
+    // post kernels' loops)
+    constexpr int NT = WPE == 6 ? 768 : BT_THREADS;
+    const int tid = threadIdx.x;
     const int l = tid % LB;
     const int gid = tid / LB, NG = NT / LB;
     const int gbase = (tid & 63) - l;       // first lane of my group in the wave
@@ -1637,8 +1642,9 @@ static void launch_lb(const DevGraph& g, const DevTable& tab, const BatchScratch
                       int grid) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_batch_rows<LB, WPE, GB, PART>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, cfg.ldsBytes);
-    hipLaunchKernelGGL((k_batch_rows<LB, WPE, GB, PART>), dim3(grid), dim3(cfg.threads), cfg.ldsBytes, st, g,
-                       tab, bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
+    // (the kernel's NT is compile-time: the variant's own size, batch_threads)
+    hipLaunchKernelGGL((k_batch_rows<LB, WPE, GB, PART>), dim3(grid), dim3(batch_threads(WPE)), cfg.ldsBytes,
+                       st, g, tab, bs, dBatchRows, nBatches, dRowAmbig, cfg.delta, dDbg, tie);
 }
 
 // The cooperative relax (PART 3) exists for LB 8 and 16 with LDS bitmaps --
@@ -1662,7 +1668,7 @@ static int launch_coop_lb(const DevGraph& g, const DevTable& tab, const BatchScr
     int32_t* a7 = dDbg;
     const TieBuf* a8 = tie;
     void* args[] = {&a0, &a1, &a2, &a3, &a4, &a5, &a6, &a7, &a8};
-    return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(cfg.threads), args, (unsigned)cfg.ldsBytes, st) ==
+    return hipLaunchCooperativeKernel(fn, dim3(grid), dim3(batch_threads(WPE)), args, (unsigned)cfg.ldsBytes, st) ==
                    hipSuccess
                ? 0
                : -1;

@@ -83,7 +83,7 @@ struct Tuning {
     int spThreads = 512, heavyDeg = 64, layout = -1, wgPerCU = 8, kflags = 0;
     double deltaFactor = 16.0;
     int exactHc = 0, exactPerCU = 0;
-    int batch = -1, batchLB = 0, batchThreads = 1024, batchGrid = 0, batchOrder = 1, batchWpe = 0;
+    int batch = -1, batchLB = 0, batchGrid = 0, batchOrder = 1, batchWpe = 0;
     int relabel = 1;           // batched path: 1 = device ids by descending degree, 0 = as given
     int batchSplit = 1;        // batched path: relax / post as two kernels (predecessors on demand)
     double batchDeltaFactor = 0.75, batchScratchGB = 64.0;

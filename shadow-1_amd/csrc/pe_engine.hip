@@ -170,7 +170,6 @@ static void read_tuning(Tuning& t, int32_t flags) {
     gi("SHDPE_EXACT_PER_CU", t.exactPerCU);
     gi("SHDPE_BATCH", t.batch);
     gi("SHDPE_BATCH_LB", t.batchLB);
-    gi("SHDPE_BATCH_THREADS", t.batchThreads);
     gi("SHDPE_BATCH_GRID", t.batchGrid);
     gi("SHDPE_BATCH_ORDER", t.batchOrder);
     gi("SHDPE_BATCH_WPE", t.batchWpe);
@@ -308,8 +307,8 @@ static int configure(ShdPe* pe, Shard* sh) {
     b.lb = tu.batchLB;
     if (b.lb != 4 && b.lb != 8 && b.lb != 16 && b.lb != 32)
         b.lb = ((int64_t)sh->rowCount + 15) / 16 >= (int64_t)sh->numCUs ? 16 : 8;
-    b.threads = tu.batchThreads;
-    if (b.threads != 256 && b.threads != 512) b.threads = 1024;
+    // (1024 threads, 768 for the 6-wave variant: compile-time in the kernel)
+    b.threads = batch_threads(8);
     // pending bitmaps (2 x n/8 bytes) in LDS while they fit beside the
     // control block, else in each slot's global scratch (gbits, LB 16)
     b.gbits = pe->batched && batch_lds_bytes((int)n, 8, false) > LDS ? 1 : 0;
