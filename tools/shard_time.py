@@ -11,7 +11,9 @@ wl = sys.argv[1]
 top, att = G.make_config(wl)
 for N in [int(x) for x in sys.argv[2:]]:
     dbg = DEBUG_ENV if any(k.startswith("SHDPE_") for k in os.environ) else 0
-    eng = Engine(top, att, shard_index=0, shard_count=N, debug_flags=dbg)
+    K = int(os.environ.get("SUBK", "1"))     # row shards per GPU on concurrent streams
+    eng = Engine(top, att, shard_index=0, shard_count=N, debug_flags=dbg,
+                 devices=[0] * K if K > 1 else None)
     s0, cnt = eng.owned
     pos = np.arange(s0, s0 + cnt, dtype=np.int32)
     eng.tune()                               # as bench.py: per-box kernel variants
@@ -28,5 +30,5 @@ for N in [int(x) for x in sys.argv[2:]]:
           f"waves={st['batchWaves']}/{st['batchPostWaves']} coop={st.get('batchCoop', 0)} "
           f"aborts={st.get('relaxCoopAborts', 0)} exact={st['rowsExact']} "
           f"rows/s/gpu={cnt/best:.0f} -> {N*cnt/best:.0f} total "
-          f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('SHDPE_'))}]", flush=True)
+          f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('SHDPE_') or k == 'SUBK')}]", flush=True)
     eng.close()
