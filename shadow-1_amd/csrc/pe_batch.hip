@@ -512,6 +512,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         __syncthreads();
 #endif
         uint32_t needMask = 0u;
+        bool lastFull = true;     // the final attempt ran the full predecessor pass
         for (int attempt = 0;; ++attempt) {
         const bool fullPred = PT != 2 || attempt > 0;
         if (attempt > 0) DIAG_WHY(64u);
@@ -1533,8 +1534,15 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         __syncthreads();
         if (tid == 0) ctl->ambMask = 0u;
         __syncthreads();
-        // a tie row's export needs every vertex's parent: the full pass
-        if (!fullPred && !failed && (retry || needMask)) continue;
+        // a tie row's export needs every vertex's parent: the full pass --
+        // in line, or (the post kernel, with a deferred-export buffer) by
+        // k_tie_export over the whole GPU after this kernel, so a tie batch
+        // no longer runs a second full pass here (round 6: the c4q post
+        // kernel was 43 vs 31 ms, a tie batch's in-line pass on its tail)
+        const bool deferTie = PT == 2 && tieDesc != nullptr &&
+                              __builtin_amdgcn_readfirstlane((int)(ld_wg(&tieDesc->req) != nullptr)) != 0;
+        if (!fullPred && !failed && (retry || (needMask && !deferTie))) continue;
+        lastFull = fullPred;
         break;
         }   // attempts
         if constexpr (PT == 1) {
@@ -1561,6 +1569,9 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             // descriptor read from memory here only: as a kernel argument
             // it cost the hot loops registers (SGPR spills)
             const TieBuf tie = *tieDesc;
+            // deferred (attempt 0 of the post kernel): the slot records the
+            // request, k_tie_export fills it after this kernel
+            const bool defer = PT == 2 && !lastFull;
             if (tid < LB) {
                 int sl = -1;
                 if ((needMask >> tid) & 1u) {
@@ -1569,9 +1580,16 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
                 }
                 tieSlot[tid] = sl;
                 tieThr[tid] = 0ull;
+                if (defer && sl >= 0) {       // thread tid < LB is lane tid of group 0
+                    tie.thr[sl] = 0.0;
+                    tie.req[4 * sl + 0] = b;
+                    tie.req[4 * sl + 1] = tid;
+                    tie.req[4 * sl + 2] = src;
+                    tie.req[4 * sl + 3] = *tie.round;
+                }
             }
             __syncthreads();
-            const int sl = tieSlot[l];
+            const int sl = defer ? -1 : tieSlot[l];
             unsigned long long thr = 0ull;
             for (int v = gid; v < n; v += NG) {
                 if (sl < 0) continue;
@@ -1598,7 +1616,7 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
             if (thr) atomicMax(&tieThr[l], thr);
             fence_wg();
             __syncthreads();
-            if (gid == 0 && sl >= 0) tie.thr[sl] = b2d(tieThr[l]);
+            if (!defer && gid == 0 && sl >= 0) tie.thr[sl] = b2d(tieThr[l]);
         } else if (tid < LB) {
             tieSlot[tid] = -1;
         }
@@ -1633,6 +1651,83 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
         __syncthreads();
         if (dbg && tid == 0) dbg[16 * b + 8] = (int)(((long long)clock64() - ctl->t4) >> 10);
     }
+}
+
+// k_tie_export: the deferred tie export of one round (launch_tie_export).
+// One thread per (slot, vertex), grid-stride: the vertex's distance, and its
+// parent exactly as the post kernel's full predecessor pass derives it (first
+// in-arc, in incidence order, among the tight ones with minimum dist[u];
+// TIE_AMB on equal minima or a zero-increment arc; -1 for the source and
+// unreachable vertices), the threshold as the maximum tied-predecessor
+// distance over the ambiguous entries (k_exact_rows' early stop), and the
+// Bellman check over every in-arc (a violation sends the row to the full
+// emulation, rowAmbig 1, as a failed batch would).
+template <int LB>
+__global__ __launch_bounds__(256) void k_tie_export(DevGraph g0, BatchScratch bs, TieBuf tie, int round,
+                                                    uint8_t* __restrict__ rowAmbig) {
+    const DevGraph g = global_view(g0);
+    const int n = g.n;
+    const bool undirected = g.inCol == g.col;
+    const int cnt = min(*as_global(tie.count), tie.cap);
+    const size_t SE = (size_t)bs.nStride * LB;
+    const size_t total = (size_t)cnt * (size_t)n;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        const int sl = (int)(i / (size_t)n);
+        const int v = (int)(i % (size_t)n);
+        const int32_t* rq = as_global(tie.req) + 4 * sl;
+        if (rq[3] != round) continue;
+        const int b = rq[0], l = rq[1], src = rq[2];
+        const unsigned long long* D = as_global(bs.D) + (size_t)b * SE;
+        const unsigned long long dv = dec(D[(size_t)v * LB + l]);
+        const size_t o = (size_t)sl * (size_t)tie.n + v;
+        as_global(tie.D)[o] = b2d(dv);
+        int pe = -1;
+        if (v != src) {
+            const int a0 = undirected ? g.rowPtr[v] : g.inPtr[v];
+            const int a1 = undirected ? g.rowPtr[v + 1] : g.inPtr[v + 1];
+            unsigned long long best = INF_BITS, mn = INF_BITS;
+            int cnt2 = 0, ba = -1;
+            for (int a = a0; a < a1; ++a) {
+                const int u = undirected ? g.col[a] : g.inCol[a];
+                const double w = undirected ? g.lat[a] : g.inLat[a];
+                const unsigned long long du = dec(D[(size_t)u * LB + l]);
+                const double cand = b2d(du) + w;
+                const unsigned long long cb = d2b(cand);
+                mn = cb < mn ? cb : mn;
+                if (dv != INF_BITS && du <= dv && cand == b2d(dv)) {
+                    if (du < best) {
+                        best = du;
+                        cnt2 = 1;
+                        ba = a;
+                    } else if (du == best) {
+                        ++cnt2;
+                    }
+                }
+            }
+            if (mn < dv) rowAmbig[(size_t)b * LB + l] = 1;   // Bellman violation: full emulation
+            if (dv != INF_BITS) {
+                const bool ea = cnt2 != 1 || best == dv;
+                pe = ea ? (TIE_AMB | (ba > 0 ? ba : 0)) : ba;
+                if (ea && best != INF_BITS)
+                    atomicMax(reinterpret_cast<unsigned long long*>(as_global(tie.thr) + sl), best);
+            }
+        }
+        as_global(tie.P)[o] = pe;
+    }
+}
+
+void launch_tie_export(const DevGraph& g, const BatchScratch& bs, int lb, const TieBuf& tie, int round,
+                       uint8_t* dRowAmbig, int grid, void* stream) {
+    if (tie.cap <= 0 || !tie.req) return;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (lb == 4)
+        hipLaunchKernelGGL(k_tie_export<4>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
+    else if (lb == 8)
+        hipLaunchKernelGGL(k_tie_export<8>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
+    else if (lb == 32)
+        hipLaunchKernelGGL(k_tie_export<32>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
+    else
+        hipLaunchKernelGGL(k_tie_export<16>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
 }
 
 template <int LB, int WPE, bool GB, int PART>

@@ -179,6 +179,12 @@ struct TieBuf {
     int32_t* H;              // [cap][n] k_tie_write hop labels
     double* R;               // [cap][n] k_tie_write reliability labels
     int64_t n;
+    // deferred export (k_batch_rows post kernel -> k_tie_export): per slot
+    // {batch within its round, lane, source, round}; `round` = the device
+    // word the host sets to the round whose post kernel runs (null: the
+    // post kernel exports in line, after a full predecessor pass)
+    int32_t* req;            // [cap][4]
+    int32_t* round;
 };
 
 // per-entry flags (mirror SHD_PE_F_* in include/shd_pathengine.h)
@@ -258,6 +264,14 @@ int launch_batch_relax_coop(const DevGraph& g, const DevTable& tab, const BatchS
                             const BatchLaunch& cfg, int32_t* dDbg, const TieBuf* tie, void* stream);
 const void* batch_coop_kernel_ptr(int lb, int wpe);
 int batch_lds_bytes(int n, int wpe, bool gbits);
+// Deferred tie export of one round (after its post kernel): for every slot
+// the post kernel requested in round `round`, the tie data of the lane's row
+// -- every vertex's distance, its igraph parent (first tight in-arc of
+// minimum dist[u], TIE_AMB on equal minima or a zero-increment arc) and the
+// tie threshold -- from the round's persisted distance array, over the whole
+// GPU; a Bellman violation sends the row to the full emulation (rowAmbig 1).
+void launch_tie_export(const DevGraph& g, const BatchScratch& bs, int lb, const TieBuf& tie,
+                       int round, uint8_t* dRowAmbig, int grid, void* stream);
 int batch_threads(int wpe);    // workgroup size of a variant (6 waves: 768, else 1024)
 int64_t batch_bits_words(int n);   // per slot, both bitmaps
 // batched helpers (pe_aux.hip), all on `stream`

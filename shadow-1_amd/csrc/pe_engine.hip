@@ -878,16 +878,19 @@ static int ensure_tie(ShdPe* pe, Shard* sh) {
     size_t cap = std::min<size_t>({(size_t)254, (size_t)sh->rowsCap, ((size_t)2 << 30) / perTie});
     if (pe->hg.nArcs() >= ((int64_t)1 << 30)) cap = 0;
     if (cap > 0) {
-        void *td, *tp, *th, *tr, *tt, *tc, *sl, *dd;
+        void *td, *tp, *th, *tr, *tt, *tc, *sl, *dd, *rq;
         const size_t cn = cap * (size_t)pe->hg.n;
         if ((rc = dev_alloc(sh, &td, cn * 8)) || (rc = dev_alloc(sh, &tp, cn * 4)) ||
             (rc = dev_alloc(sh, &th, cn * 4)) || (rc = dev_alloc(sh, &tr, cn * 8)) ||
             (rc = dev_alloc(sh, &tt, cap * 8)) || (rc = dev_alloc(sh, &tc, 16)) ||
             (rc = dev_alloc(sh, &sl, (size_t)sh->rowsCap * 4)) ||
-            (rc = dev_alloc(sh, &dd, sizeof(TieBuf))))
+            (rc = dev_alloc(sh, &dd, sizeof(TieBuf))) || (rc = dev_alloc(sh, &rq, cap * 16)))
             return rc;
+        // (tc: [0] slot counter, [1] the round word of the deferred export;
+        // the batched path's post kernel defers its export to k_tie_export)
         sh->tie = TieBuf{(int32_t)cap, (int32_t*)tc, (double*)td, (int32_t*)tp, (double*)tt,
-                         (int32_t*)th, (double*)tr, (int64_t)pe->hg.n};
+                         (int32_t*)th, (double*)tr, (int64_t)pe->hg.n,
+                         pe->batched ? (int32_t*)rq : nullptr, (int32_t*)tc + 1};
         sh->dSlots = (int32_t*)sl;
         sh->dTie = (TieBuf*)dd;
         HIPCHK(hipMemcpy(sh->dTie, &sh->tie, sizeof(TieBuf), hipMemcpyHostToDevice));
@@ -1300,6 +1303,15 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                         if (part == 1 && pe->tu.failWpe && relax.wpe == pe->tu.failWpe)
                             HIPCHK(hipMemsetAsync(sh->bsc.flags, 1, (size_t)rn * 4, sh->stream));
                         if (sh->timeParts) HIPCHK(hipEventRecord(sh->evP[part], sh->stream));
+                        // the post kernel's deferred tie export of this round
+                        // (the round's dist arrays persist until the next
+                        // round's relax)
+                        if (part == 1 && sh->tie.req)
+                            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)sh->tie.round, r0 / sh->batchRound, 1,
+                                                     sh->stream));
+                        if (part == 2 && sh->tie.req)
+                            launch_tie_export(sh->dg, sh->bsc, LB, sh->tie, r0 / sh->batchRound,
+                                              sh->dBatchAmb + ro, sh->numCUs * 4, sh->stream);
                     }
                     if (sh->timeParts) {
                         HIPCHK(hipEventSynchronize(sh->evP[2]));
