@@ -1661,10 +1661,11 @@ void k_batch_rows(DevGraph g0, DevTable tab0,
 // unreachable vertices), the threshold as the maximum tied-predecessor
 // distance over the ambiguous entries (k_exact_rows' early stop), and the
 // Bellman check over every in-arc (a violation sends the row to the full
-// emulation, rowAmbig 1, as a failed batch would).
+// emulation, rowAmbig 1, as a failed batch would).  violSlot >= 0 (tests,
+// SHDPE_TIE_CORRUPT=3): that slot's row is treated as violated.
 template <int LB>
 __global__ __launch_bounds__(256) void k_tie_export(DevGraph g0, BatchScratch bs, TieBuf tie, int round,
-                                                    uint8_t* __restrict__ rowAmbig) {
+                                                    uint8_t* __restrict__ rowAmbig, int violSlot) {
     const DevGraph g = global_view(g0);
     const int n = g.n;
     const bool undirected = g.inCol == g.col;
@@ -1704,7 +1705,7 @@ __global__ __launch_bounds__(256) void k_tie_export(DevGraph g0, BatchScratch bs
                     }
                 }
             }
-            if (mn < dv) rowAmbig[(size_t)b * LB + l] = 1;   // Bellman violation: full emulation
+            if (mn < dv || sl == violSlot) rowAmbig[(size_t)b * LB + l] = 1;   // Bellman violation: full emulation
             if (dv != INF_BITS) {
                 const bool ea = cnt2 != 1 || best == dv;
                 pe = ea ? (TIE_AMB | (ba > 0 ? ba : 0)) : ba;
@@ -1717,17 +1718,17 @@ __global__ __launch_bounds__(256) void k_tie_export(DevGraph g0, BatchScratch bs
 }
 
 void launch_tie_export(const DevGraph& g, const BatchScratch& bs, int lb, const TieBuf& tie, int round,
-                       uint8_t* dRowAmbig, int grid, void* stream) {
+                       uint8_t* dRowAmbig, int grid, int violSlot, void* stream) {
     if (tie.cap <= 0 || !tie.req) return;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (lb == 4)
-        hipLaunchKernelGGL(k_tie_export<4>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
+        hipLaunchKernelGGL(k_tie_export<4>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig, violSlot);
     else if (lb == 8)
-        hipLaunchKernelGGL(k_tie_export<8>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
+        hipLaunchKernelGGL(k_tie_export<8>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig, violSlot);
     else if (lb == 32)
-        hipLaunchKernelGGL(k_tie_export<32>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
+        hipLaunchKernelGGL(k_tie_export<32>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig, violSlot);
     else
-        hipLaunchKernelGGL(k_tie_export<16>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig);
+        hipLaunchKernelGGL(k_tie_export<16>, dim3(grid), dim3(256), 0, st, g, bs, tie, round, dRowAmbig, violSlot);
 }
 
 template <int LB, int WPE, bool GB, int PART>

@@ -91,8 +91,9 @@ struct Tuning {
     int densePredMi = 2, denseEpochs = 1;
     int debug = 0, streamWgPerCU = 16;
     int tuneLog = 0;           // print shd_pe_tune's per-variant times (no kernel counters)
-    int tieCorrupt = 0;        // tests only: scale one early-stop slot's exported distances
-                               // after the relevance scan (exercises the tie-slot repair)
+    int tieCorrupt = 0;        // tests only: 1 / 2 scale one early-stop slot's exported
+                               // distances after the relevance scan (exercises the tie-slot
+                               // repair); 3 = k_tie_export treats its first slot as violated
     int batchCoop = 0;         // cooperative relax: K workgroups per batch (>= 2 forces it,
                                // 1 = a shd_pe_tune candidate, 0 = off)
     int batchCoopWpe = 0;      // its variant (8 / 6 / 4 waves; 0 = the one with two
@@ -269,9 +270,10 @@ int batch_lds_bytes(int n, int wpe, bool gbits);
 // -- every vertex's distance, its igraph parent (first tight in-arc of
 // minimum dist[u], TIE_AMB on equal minima or a zero-increment arc) and the
 // tie threshold -- from the round's persisted distance array, over the whole
-// GPU; a Bellman violation sends the row to the full emulation (rowAmbig 1).
+// GPU; a Bellman violation sends the row to the full emulation (rowAmbig 1;
+// violSlot >= 0: tests, that slot's row is treated as violated).
 void launch_tie_export(const DevGraph& g, const BatchScratch& bs, int lb, const TieBuf& tie,
-                       int round, uint8_t* dRowAmbig, int grid, void* stream);
+                       int round, uint8_t* dRowAmbig, int grid, int violSlot, void* stream);
 int batch_threads(int wpe);    // workgroup size of a variant (6 waves: 768, else 1024)
 int64_t batch_bits_words(int n);   // per slot, both bitmaps
 // batched helpers (pe_aux.hip), all on `stream`

@@ -1311,7 +1311,8 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                                                      sh->stream));
                         if (part == 2 && sh->tie.req)
                             launch_tie_export(sh->dg, sh->bsc, LB, sh->tie, r0 / sh->batchRound,
-                                              sh->dBatchAmb + ro, sh->numCUs * 4, sh->stream);
+                                              sh->dBatchAmb + ro, sh->numCUs * 4,
+                                              pe->tu.tieCorrupt == 3 ? 0 : -1, sh->stream);
                     }
                     if (sh->timeParts) {
                         HIPCHK(hipEventSynchronize(sh->evP[2]));
@@ -1420,7 +1421,8 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 return rc;
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             if (nTie > 0) launch_tie_scan(sh->dg, sh->dRows, sh->dSlots, nTie, sh->tie, sh->stream);
-            if (nTie > 0 && pe->tu.tieCorrupt) corrupt_tie_slot(pe, sh, exactSlots, nTie);
+            if (nTie > 0 && (pe->tu.tieCorrupt == 1 || pe->tu.tieCorrupt == 2))
+                corrupt_tie_slot(pe, sh, exactSlots, nTie);
             if (dense)      // ~n arcs per pop: the workgroup-wide scan
                 launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
                                    sh->exactGrid, sh->exactHc, sh->dXList, sh->stream);

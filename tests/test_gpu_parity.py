@@ -834,6 +834,22 @@ def test_tie_slot_cross_check_repairs(E, oracle_mod, monkeypatch, case, mode):
     assert st["rowsTieEarly"] > 0 and st["rowsTieRepaired"] >= 1, st
 
 
+def test_deferred_tie_export_violation_takes_full_emulation(E, oracle_mod, monkeypatch):
+    """The batched path's deferred tie export (k_tie_export, after the post
+    kernel) re-checks every in-arc of every vertex of a tie row's distance
+    array; a Bellman violation there must send that row to the full igraph
+    emulation instead of the early-stop one.  SHDPE_TIE_CORRUPT=3 makes the
+    export treat its first slot as violated: one early-stop row fewer, the
+    same rows to the exact path, every row still bit-exact with the oracle."""
+    top, att = G.random_sparse(600, 6, seed=216, quantum=1.0), np.arange(599)
+    base = _check_engine(E, oracle_mod, top, att, force=5, debug_flags=E.DEBUG_ENV)
+    monkeypatch.setenv("SHDPE_TIE_CORRUPT", "3")
+    st = _check_engine(E, oracle_mod, top, att, force=5, debug_flags=E.DEBUG_ENV)
+    assert base["rowsTieEarly"] >= 1, base
+    assert st["rowsExact"] == base["rowsExact"], (base, st)
+    assert st["rowsTieEarly"] == base["rowsTieEarly"] - 1, (base, st)
+
+
 def test_tune_with_fewer_scratch_slots_than_grid(E, oracle_mod, monkeypatch):
     """A scratch budget below the resident grid (huge graphs, or a small
     SHDPE_BATCH_SCRATCH_GB): shd_pe_tune must time its variants -- and keep
