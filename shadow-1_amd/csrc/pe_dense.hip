@@ -348,6 +348,70 @@ void launch_dense_build(const DevGraph& g, double* W, double* Rl, int64_t n, int
                            g, W, Rl, n);
 }
 
+// Early-stop tie slots of dense tie rows (round 6; undirected graphs, whose
+// in-arcs are the vertex's own arc row sorted by neighbour).  From the
+// converged distance row and the predecessor pass's choice per entry: the
+// row's distances; its parents as in-arc indices -- the unique minimum u's
+// arc u -> v, or, where the pass saw equal minima or a zero increment, the
+// first tight arc of minimum dist[u] flagged TIE_AMB, whose tied distance
+// raises the slot's threshold (atomic max on the f64 bits; the host zeroes
+// it first) -- for k_tie_scan, k_exact_dense's early stop and k_tie_write.
+// dIdx: the row of D / P per slot, pos: its table position.
+__global__ __launch_bounds__(256) void k_dense_tie_export(DevGraph g, const double* D, const int32_t* P,
+                                                          int64_t n, int64_t ldD,
+                                                          const int32_t* __restrict__ dIdx,
+                                                          const int32_t* __restrict__ pos, TieBuf tie) {
+    const int sl = blockIdx.y;
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= n) return;
+    const int64_t b = dglobal(dIdx)[sl];
+    const int s = dglobal(g.attached)[dglobal(pos)[sl]];
+    const double* Db = dglobal(D) + b * ldD;
+    const double d = Db[v];
+    const int p = dglobal(P)[b * ldD + v];
+    int pe = -1;
+    if (v != s && d < DINF) {
+        const int a0 = dglobal(g.rowPtr)[v], a1 = dglobal(g.rowPtr)[v + 1];
+        if (p >= 0 && !(Db[p] == d)) {                  // unique minimum, positive increment
+            if (a1 - a0 == n - 1) {
+                pe = a0 + (p < v ? p : p - 1);
+            } else {
+                int lo = a0, hi = a1;
+                while (lo < hi) {
+                    const int mid = lo + ((hi - lo) >> 1);
+                    if (dglobal(g.col)[mid] < p) lo = mid + 1; else hi = mid;
+                }
+                pe = lo;
+            }
+        } else {                                        // ambiguous: the heap decides
+            double best = DINF;
+            int ba = -1;
+            for (int a = a0; a < a1; ++a) {
+                const double du = Db[dglobal(g.col)[a]];
+                if (du <= d && du + dglobal(g.lat)[a] == d && du < best) {
+                    best = du;
+                    ba = a;
+                }
+            }
+            pe = TIE_AMB | (ba > 0 ? ba : 0);
+            if (best < DINF)
+                atomicMax(reinterpret_cast<unsigned long long*>(dglobal(tie.thr) + sl),
+                          (unsigned long long)__double_as_longlong(best));
+        }
+    }
+    dglobal(tie.D)[(size_t)sl * (size_t)tie.n + v] = d;
+    dglobal(tie.P)[(size_t)sl * (size_t)tie.n + v] = pe;
+}
+
+void launch_dense_tie_export(const DevGraph& g, const double* D, const int32_t* P, int64_t n,
+                             const int32_t* dIdx, const int32_t* dPos, const TieBuf& tie, int32_t nSlots,
+                             void* stream) {
+    if (nSlots <= 0) return;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_dense_tie_export, dim3((unsigned)((n + 255) / 256), (unsigned)nSlots), dim3(256), 0,
+                       st, g, D, P, n, n, dIdx, dPos, tie);
+}
+
 int launch_dense_rows(const DevGraph& g, const DevTable& tab, const double* W, const double* Rl,
                       double* D, int32_t* P, uint8_t* rowActive, uint8_t* rowChanged,
                       uint8_t* rowAmb, int32_t* dAny, uint8_t* chunkEpoch, const int32_t* dRows,

@@ -232,7 +232,13 @@ int exact_soa_max_n();
 // slot `stride` entries of exact_dense_list_bytes()
 void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc, void* dList,
-                        void* stream);
+                        const int32_t* dSlots, const TieBuf& tie, void* stream);
+// early-stop tie slots 0 .. nSlots-1 of dense tie rows (undirected graphs):
+// distances, in-arc parents (TIE_AMB where the heap decides) and thresholds
+// from the min-plus D / P rows dIdx[k] of table positions dPos[k]
+void launch_dense_tie_export(const DevGraph& g, const double* D, const int32_t* P, int64_t n,
+                             const int32_t* dIdx, const int32_t* dPos, const TieBuf& tie, int32_t nSlots,
+                             void* stream);
 int exact_dense_list_bytes();
 // tie rows whose ambiguous entries lie on no target's path: thr := -1 (the
 // exact kernel then keeps the fast-path parents)

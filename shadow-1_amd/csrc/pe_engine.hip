@@ -87,6 +87,7 @@ struct Shard {
     TieBuf tie{};                   // early-stop tie rows (batched path)
     int32_t* dSlots = nullptr;      // per exact row its tie slot, -1 full emulation
     TieBuf* dTie = nullptr;         // device copy of `tie` (k_batch_rows reads it)
+    int32_t* dDenseIdx = nullptr;   // dense early-stop tie rows: their row of the D / P matrices
     long long* dXdbg = nullptr;     // exact-kernel counters (SHD_PE_DEBUG_COUNTERS)
     bool tieTried = false;
     double *dW = nullptr, *dRl = nullptr, *dD = nullptr;
@@ -1186,6 +1187,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
     if (rc) return rc;
     std::vector<uint8_t> amb;
     std::vector<int32_t> exactRows, exactSlots, fullRows;
+    std::vector<int32_t> denseIdx;   // dense tie rows: their row of D / P (one dense chunk only)
     ShdPeStats& st = sh->stats;
     HIPCHK(hipEventRecord(sh->ev0, sh->stream));
     for (int32_t c0 = 0; c0 < count; c0 += sh->rowsCap) {
@@ -1194,6 +1196,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                               sh->stream));
         exactRows.clear();
         exactSlots.clear();
+        denseIdx.clear();
         if (pe->mode == 2) {
             HIPCHK(hipEventRecord(sh->evA, sh->stream));
             launch_direct_rows(sh->dg, sh->tab, sh->dRows, cnt, sh->stream);
@@ -1230,7 +1233,10 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 st.denseSweeps += sweeps;
                 st.denseFlops += flops;
                 for (int32_t i = 0; i < dc; ++i)
-                    if (amb[i]) exactRows.push_back(pos[c0 + d0 + i]);
+                    if (amb[i]) {
+                        exactRows.push_back(pos[c0 + d0 + i]);
+                        if (dc == cnt) denseIdx.push_back(i);   // D / P still hold the row
+                    }
             }
         } else if (pe->batched) {
             if ((rc = ensure_batch(pe, sh))) return rc;
@@ -1403,6 +1409,72 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 print_sparse_debug(pe, sh, dbg.data(), cnt);
             }
         }
+        // Dense tie rows with early stop (round 6; undirected graphs whose rows
+        // fit one dense chunk, so D / P still hold them): in groups of the
+        // tie slots, each row's slot filled from D / P (k_dense_tie_export),
+        // the relevance scan, the emulation only until the row's tied
+        // predecessors are popped (k_exact_dense) and k_tie_write.  A slot
+        // failing the emulation's consistency check is redone in full.
+        if (!exactRows.empty() && pe->mode == 3 && pe->opt.forceMode != 3 && !pe->hg.latFold &&
+            !pe->hg.directed && denseIdx.size() == exactRows.size()) {
+            if ((rc = ensure_tie(pe, sh))) return rc;
+            if (sh->tie.cap > 0 && !sh->dDenseIdx) {
+                void* di;
+                if ((rc = dev_alloc(sh, &di, (size_t)sh->rowsCap * 4))) return rc;
+                sh->dDenseIdx = (int32_t*)di;
+            }
+            if (sh->tie.cap > 0) {
+                if (!sh->dXList &&
+                    (rc = dev_alloc(sh, &sh->dXList, (size_t)sh->exactGrid * (size_t)sh->sc.stride *
+                                                         (size_t)exact_dense_list_bytes())))
+                    return rc;
+                const int32_t cap = sh->tie.cap;
+                std::vector<int32_t> slots(cap), redo;
+                for (int32_t k = 0; k < cap; ++k) slots[k] = k;
+                HIPCHK(hipMemcpyAsync(sh->dSlots, slots.data(), (size_t)cap * 4, hipMemcpyHostToDevice,
+                                      sh->stream));
+                HIPCHK(hipEventRecord(sh->evA, sh->stream));
+                for (size_t g0 = 0; g0 < exactRows.size(); g0 += (size_t)cap) {
+                    const int32_t k = (int32_t)std::min<size_t>(cap, exactRows.size() - g0);
+                    HIPCHK(hipMemcpyAsync(sh->dRows, exactRows.data() + g0, (size_t)k * 4,
+                                          hipMemcpyHostToDevice, sh->stream));
+                    HIPCHK(hipMemcpyAsync(sh->dDenseIdx, denseIdx.data() + g0, (size_t)k * 4,
+                                          hipMemcpyHostToDevice, sh->stream));
+                    HIPCHK(hipMemsetAsync(sh->tie.thr, 0, (size_t)k * 8, sh->stream));
+                    launch_dense_tie_export(sh->dg, sh->dD, sh->dP, pe->hg.n, sh->dDenseIdx, sh->dRows, sh->tie,
+                                            k, sh->stream);
+                    launch_tie_scan(sh->dg, sh->dRows, sh->dSlots, k, sh->tie, sh->stream);
+                    launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, k, sh->exactGrid, sh->exactHc,
+                                       sh->dXList, sh->dSlots, sh->tie, sh->stream);
+                    launch_tie_write(sh->dg, sh->tab, sh->dRows, sh->dSlots, k, sh->tie, sh->stream);
+                    HIPCHK(hipGetLastError());
+                    std::vector<double> thr((size_t)k);
+                    HIPCHK(hipMemcpyAsync(thr.data(), sh->tie.thr, (size_t)k * 8, hipMemcpyDeviceToHost,
+                                          sh->stream));
+                    HIPCHK(hipStreamSynchronize(sh->stream));
+                    for (int32_t i = 0; i < k; ++i)
+                        if (std::isnan(thr[(size_t)i])) redo.push_back(exactRows[g0 + (size_t)i]);
+                    st.rowsTieEarly += k;
+                }
+                if (!redo.empty()) {
+                    std::fprintf(stderr, "[shdpe] shard %d: %zu dense early-stop tie row(s) failed the slot "
+                                 "consistency check; recomputed by the full emulation\n",
+                                 sh->gindex, redo.size());
+                    HIPCHK(hipMemcpyAsync(sh->dRows, redo.data(), redo.size() * 4, hipMemcpyHostToDevice,
+                                          sh->stream));
+                    launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)redo.size(),
+                                       sh->exactGrid, sh->exactHc, sh->dXList, nullptr, sh->tie, sh->stream);
+                    HIPCHK(hipGetLastError());
+                    st.rowsTieRepaired += (int64_t)redo.size();
+                }
+                HIPCHK(hipEventRecord(sh->evB, sh->stream));
+                HIPCHK(hipEventSynchronize(sh->evB));
+                st.msExactKernel += elapsed(sh->evA, sh->evB);
+                st.launchesExact++;
+                st.rowsExact += (int64_t)exactRows.size();
+                exactRows.clear();
+            }
+        }
         if (!exactRows.empty()) {
             HIPCHK(hipMemcpyAsync(sh->dRows, exactRows.data(), exactRows.size() * 4,
                                   hipMemcpyHostToDevice, sh->stream));
@@ -1425,7 +1497,7 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 corrupt_tie_slot(pe, sh, exactSlots, nTie);
             if (dense)      // ~n arcs per pop: the workgroup-wide scan
                 launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
-                                   sh->exactGrid, sh->exactHc, sh->dXList, sh->stream);
+                                   sh->exactGrid, sh->exactHc, sh->dXList, nullptr, sh->tie, sh->stream);
             else
                 launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
                                   sh->exactGrid, sh->exactHc, pe->tu.exactHc > 0, dSl, sh->tie,

@@ -1770,11 +1770,17 @@ struct alignas(16) XdEntry {
     int32_t st;      // 0: push (never reached), >= 2: modify (index2 at scan time)
 };
 
+// slots (round 6): early-stop tie rows of the dense path (k_dense_tie_export
+// filled their slots): the emulation stops once the popped key passes the
+// slot's threshold and merges its parents into the slot (as k_exact_rows'
+// tie_finalize, workgroup-wide); k_tie_write then writes the row.
 __global__ __launch_bounds__(XD_THREADS) void k_exact_dense(DevGraph g0, DevTable tab0,
                                                             DevScratch sc0,
                                                             const int32_t* __restrict__ rows,
                                                             int32_t nRows, int32_t hc,
-                                                            XdEntry* __restrict__ lists) {
+                                                            XdEntry* __restrict__ lists,
+                                                            const int32_t* __restrict__ slots,
+                                                            TieBuf tie) {
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
@@ -1788,13 +1794,15 @@ __global__ __launch_bounds__(XD_THREADS) void k_exact_dense(DevGraph g0, DevTabl
     double* tailKey = reinterpret_cast<double*>(sc.heapTail) + (size_t)blockIdx.x * 2 * sc.heapStride;
     const WHeap h{tailKey, reinterpret_cast<int32_t*>(tailKey + sc.heapStride), sc.index2 + slot, hc};
     XdEntry* list = as_global(lists) + (size_t)blockIdx.x * (size_t)sc.stride;
-    __shared__ int sU, sDone, sSeg;
+    __shared__ int sU, sDone, sSeg, sBad;
     __shared__ double sMind;
     __shared__ int sCnt[XD_SCAN_WAVES];
     const int ldsLevel = 30 - __builtin_clz(hc + 1);
     for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
         const int r = rows[b];
         const int s = g.attached[r];
+        const int tslot = slots ? slots[b] : -1;
+        const double thr = tslot >= 0 ? tie.thr[tslot] : 0.0;
         for (int v = tid; v < n; v += XD_THREADS) h.I2[v] = 0;
         __syncthreads();
         if (tid == 0) {
@@ -1806,13 +1814,15 @@ __global__ __launch_bounds__(XD_THREADS) void k_exact_dense(DevGraph g0, DevTabl
         }
         __syncthreads();
         int toReach = g.T;      // wave 0's
-        int size = 1;           // wave 0's
+        int size = tslot >= 0 && !(thr >= 0.0) ? 0 : 1;   // wave 0's (thr < 0: no relevant tie)
         double km = 0.0;
         int im = 0;
         for (;;) {
             // ---- pop (wave 0): the top, the last element --------------------
             if (wave == 0) {
                 int done = size <= 0 || toReach <= 0;
+                // early stop: every tied predecessor of the row is popped
+                if (!done && tslot >= 0 && -h.lkey()[0] > thr) done = 1;
                 if (!done) {
                     const int u = __builtin_amdgcn_readfirstlane(h.lidx()[0]);
                     const double mind = -h.lkey()[0];
@@ -1906,8 +1916,30 @@ __global__ __launch_bounds__(XD_THREADS) void k_exact_dense(DevGraph g0, DevTabl
             }
         }
         __syncthreads();
-        write_row(g, tab, r, s, [&](int t) { return ld_wg(&h.I2[t]) == 1 ? d2b(ld_wg(&D[t])) : INF_BITS; },
-                  [&](int t) { return ld_wg(&H[t]); }, R, P, F_EXACT, tid, XD_THREADS);
+        if (tslot >= 0) {
+            // tie_finalize, workgroup-wide: the emulated parents of the
+            // ambiguous entries, and the popped vertices' distances checked
+            // against the slot's (a mismatch: thr := NaN, the engine redoes
+            // the row with the full emulation)
+            if (tid == 0) sBad = 0;
+            __syncthreads();
+            int32_t* tp = tie.P + (size_t)tslot * (size_t)tie.n;
+            const double* td = tie.D + (size_t)tslot * (size_t)tie.n;
+            const bool live = thr >= 0.0;
+            int bad = 0;
+            for (int v = tid; v < n; v += XD_THREADS) {
+                const int fp = tp[v];
+                const int st = live ? ld_wg(&h.I2[v]) : 0;
+                if (fp >= 0 && (fp & TIE_AMB)) tp[v] = st != 0 ? ld_wg(&P[v]) : -1;
+                if (st == 1 && ld_wg(&D[v]) != td[v]) bad = 1;
+            }
+            if (bad) sBad = 1;
+            __syncthreads();
+            if (tid == 0 && sBad) tie.thr[tslot] = __longlong_as_double(0x7ff8000000000000ll);
+        } else {
+            write_row(g, tab, r, s, [&](int t) { return ld_wg(&h.I2[t]) == 1 ? d2b(ld_wg(&D[t])) : INF_BITS; },
+                      [&](int t) { return ld_wg(&H[t]); }, R, P, F_EXACT, tid, XD_THREADS);
+        }
         __syncthreads();
     }
 }
@@ -2064,7 +2096,7 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
 
 void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc, void* dList,
-                        void* stream) {
+                        const int32_t* dSlots, const TieBuf& tie, void* stream) {
     if (nRows <= 0) return;
     if (grid > nRows) grid = nRows;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -2074,7 +2106,7 @@ void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_dense),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     hipLaunchKernelGGL(k_exact_dense, dim3(grid), dim3(XD_THREADS), bytes, st, g, tab, sc, dRows, nRows,
-                       hc, reinterpret_cast<XdEntry*>(dList));
+                       hc, reinterpret_cast<XdEntry*>(dList), dSlots, tie);
 }
 
 int exact_dense_list_bytes() { return (int)sizeof(XdEntry); }
