@@ -232,7 +232,7 @@ int exact_soa_max_n();
 // slot `stride` entries of exact_dense_list_bytes()
 void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc, void* dList,
-                        const int32_t* dSlots, const TieBuf& tie, void* stream);
+                        const int32_t* dSlots, const TieBuf& tie, int32_t* dTake, void* stream);
 // early-stop tie slots 0 .. nSlots-1 of dense tie rows (undirected graphs):
 // distances, in-arc parents (TIE_AMB where the heap decides) and thresholds
 // from the min-plus D / P rows dIdx[k] of table positions dPos[k]

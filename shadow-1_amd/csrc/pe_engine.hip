@@ -876,7 +876,10 @@ static int ensure_tie(ShdPe* pe, Shard* sh) {
     sh->tieTried = true;
     int rc;
     const size_t perTie = (size_t)pe->hg.n * 24;
-    size_t cap = std::min<size_t>({(size_t)254, (size_t)sh->rowsCap, ((size_t)2 << 30) / perTie});
+    // (the dense path, mode 3, keeps slots out of rowAmbig's byte: more of them,
+    // so its early-stop tie rows run in one launch)
+    size_t cap = std::min<size_t>({pe->mode == 3 ? (size_t)4096 : (size_t)254, (size_t)sh->rowsCap,
+                                   ((size_t)2 << 30) / perTie});
     if (pe->hg.nArcs() >= ((int64_t)1 << 30)) cap = 0;
     if (cap > 0) {
         void *td, *tp, *th, *tr, *tt, *tc, *sl, *dd, *rq;
@@ -1444,8 +1447,10 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                     launch_dense_tie_export(sh->dg, sh->dD, sh->dP, pe->hg.n, sh->dDenseIdx, sh->dRows, sh->tie,
                                             k, sh->stream);
                     launch_tie_scan(sh->dg, sh->dRows, sh->dSlots, k, sh->tie, sh->stream);
+                    // rows of unequal early-stop cost: taken from a counter
+                    HIPCHK(hipMemsetAsync(sh->tie.count + 2, 0, 4, sh->stream));
                     launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, k, sh->exactGrid, sh->exactHc,
-                                       sh->dXList, sh->dSlots, sh->tie, sh->stream);
+                                       sh->dXList, sh->dSlots, sh->tie, sh->tie.count + 2, sh->stream);
                     launch_tie_write(sh->dg, sh->tab, sh->dRows, sh->dSlots, k, sh->tie, sh->stream);
                     HIPCHK(hipGetLastError());
                     std::vector<double> thr((size_t)k);
@@ -1463,7 +1468,8 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                     HIPCHK(hipMemcpyAsync(sh->dRows, redo.data(), redo.size() * 4, hipMemcpyHostToDevice,
                                           sh->stream));
                     launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)redo.size(),
-                                       sh->exactGrid, sh->exactHc, sh->dXList, nullptr, sh->tie, sh->stream);
+                                       sh->exactGrid, sh->exactHc, sh->dXList, nullptr, sh->tie, nullptr,
+                                       sh->stream);
                     HIPCHK(hipGetLastError());
                     st.rowsTieRepaired += (int64_t)redo.size();
                 }
@@ -1497,7 +1503,8 @@ static int compute_shard(ShdPe* pe, Shard* sh, const int32_t* pos, int32_t count
                 corrupt_tie_slot(pe, sh, exactSlots, nTie);
             if (dense)      // ~n arcs per pop: the workgroup-wide scan
                 launch_exact_dense(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
-                                   sh->exactGrid, sh->exactHc, sh->dXList, nullptr, sh->tie, sh->stream);
+                                   sh->exactGrid, sh->exactHc, sh->dXList, nullptr, sh->tie, nullptr,
+                                   sh->stream);
             else
                 launch_exact_rows(sh->dg, sh->tab, sh->sc, sh->dRows, (int32_t)exactRows.size(),
                                   sh->exactGrid, sh->exactHc, pe->tu.exactHc > 0, dSl, sh->tie,

@@ -1780,7 +1780,7 @@ __global__ __launch_bounds__(XD_THREADS) void k_exact_dense(DevGraph g0, DevTabl
                                                             int32_t nRows, int32_t hc,
                                                             XdEntry* __restrict__ lists,
                                                             const int32_t* __restrict__ slots,
-                                                            TieBuf tie) {
+                                                            TieBuf tie, int32_t* take) {
     const DevGraph g = global_view(g0);
     const DevTable tab = global_view(tab0);
     const DevScratch sc = global_view(sc0);
@@ -1798,7 +1798,18 @@ __global__ __launch_bounds__(XD_THREADS) void k_exact_dense(DevGraph g0, DevTabl
     __shared__ double sMind;
     __shared__ int sCnt[XD_SCAN_WAVES];
     const int ldsLevel = 30 - __builtin_clz(hc + 1);
-    for (int b = blockIdx.x; b < nRows; b += gridDim.x) {
+    // rows: static (b = blockIdx.x, + gridDim.x), or taken from a device
+    // counter (take, zeroed by the host) when early-stop rows of unequal
+    // cost run in one launch
+    __shared__ int sB;
+    for (int b = blockIdx.x;; b += gridDim.x) {
+        if (take) {
+            __syncthreads();
+            if (tid == 0) sB = atomicAdd(take, 1);
+            __syncthreads();
+            b = sB;
+        }
+        if (b >= nRows) break;
         const int r = rows[b];
         const int s = g.attached[r];
         const int tslot = slots ? slots[b] : -1;
@@ -2096,7 +2107,7 @@ void launch_exact_rows(const DevGraph& g, const DevTable& tab, const DevScratch&
 
 void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch& sc,
                         const int32_t* dRows, int32_t nRows, int32_t grid, int32_t hc, void* dList,
-                        const int32_t* dSlots, const TieBuf& tie, void* stream) {
+                        const int32_t* dSlots, const TieBuf& tie, int32_t* dTake, void* stream) {
     if (nRows <= 0) return;
     if (grid > nRows) grid = nRows;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -2106,7 +2117,7 @@ void launch_exact_dense(const DevGraph& g, const DevTable& tab, const DevScratch
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exact_dense),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     hipLaunchKernelGGL(k_exact_dense, dim3(grid), dim3(XD_THREADS), bytes, st, g, tab, sc, dRows, nRows,
-                       hc, reinterpret_cast<XdEntry*>(dList), dSlots, tie);
+                       hc, reinterpret_cast<XdEntry*>(dList), dSlots, tie, dTake);
 }
 
 int exact_dense_list_bytes() { return (int)sizeof(XdEntry); }
