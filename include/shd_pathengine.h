@@ -132,9 +132,10 @@ typedef struct ShdPeStats {
     int32_t batchLanes;        /* sources per batch (LB) when batched              */
     int32_t nShards;           /* row shards (devices) in this engine              */
     double msGather;           /* device time of shd_pe_gather                     */
-    int64_t rowsTieEarly;      /* of rowsExact: early-stop emulation (the batch
-                                  kernel exported distances, parents and the tie
-                                  threshold; k_tie_write wrote the row)          */
+    int64_t rowsTieEarly;      /* of rowsExact: early-stop emulation (distances,
+                                  parents and the tie threshold exported by the
+                                  sparse / batch kernels or, dense path,
+                                  k_dense_tie_export; k_tie_write wrote the row) */
     int32_t batchWaves;        /* k_batch_rows variant in use: waves per SIMD (4,
                                   6 or 8; shd_pe_tune picks the faster); with the
                                   split kernels, the relaxation kernel's          */
